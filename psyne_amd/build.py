@@ -1,0 +1,44 @@
+"""Build the gfx950 shared library in-tree: psyne_amd/libpsyne_tdt.so.
+
+hipcc --offload-arch=gfx950 cross-compiles without a GPU, so this runs in the build
+container; the resulting .so travels to the GPU box with the gpurun snapshot.
+"""
+from __future__ import annotations
+
+import os
+import pathlib
+import subprocess
+import sys
+
+PKG = pathlib.Path(__file__).resolve().parent
+ROOT = PKG.parent
+CSRC = PKG / "csrc"
+LIB = PKG / "libpsyne_tdt.so"
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("PSYNE_ARCH", "gfx950")
+
+SOURCES = [CSRC / "tdt_api.hip"]
+DEPS = SOURCES + [CSRC / f for f in ("tdt_device.h", "tdt_encode.h", "tdt_decode.h", "tdt_log2.h",
+                                     "glibc_log2_data.h")] + [ROOT / "include" / "psyne_tdt.h"]
+
+
+def needs_build() -> bool:
+    if not LIB.exists():
+        return True
+    t = LIB.stat().st_mtime
+    return any(p.stat().st_mtime > t for p in DEPS)
+
+
+def build(force: bool = False, verbose: bool = False) -> pathlib.Path:
+    if force or needs_build():
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+               "-I", str(ROOT / "include"), *map(str, SOURCES), "-o", str(LIB)]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.check_call(cmd)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv, verbose=True)
+    print(LIB)

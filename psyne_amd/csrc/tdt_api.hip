@@ -1,0 +1,372 @@
+// tdt_api.hip — C ABI (include/psyne_tdt.h) over the gfx950 TDT kernels.
+//
+// Build: hipcc --offload-arch=gfx950 -O3 -shared -fPIC (psyne_amd/build.py).
+// The library never falls back to a CPU path: every entry point launches a HIP kernel or
+// fails with TDT_E_HIP.
+#include "../../include/psyne_tdt.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+
+#include "tdt_decode.h"
+#include "tdt_encode.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int set_err(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIPCHK(expr)                                                                       \
+    do {                                                                                   \
+        hipError_t e_ = (expr);                                                            \
+        if (e_ != hipSuccess)                                                              \
+            return set_err(TDT_E_HIP, std::string(#expr ": ") + hipGetErrorString(e_));    \
+    } while (0)
+
+}  // namespace
+
+struct tdt_ctx {
+    int device = 0;
+    tdt_config cfg{};
+    std::atomic<double> bandwidth{100.0};  // reference defaults :352-354
+    std::atomic<double> latency{1.0};
+    std::atomic<double> cpu{0.5};
+    std::atomic<uint64_t> size_hint{65536};
+    std::mutex mu;
+    // workspace: [0..64) counters (ticket, timeout), then one u64 look-back word per message
+    uint8_t *ws = nullptr;
+    size_t ws_bytes = 0;
+    // host-path device buffers
+    uint8_t *h_dev = nullptr;
+    size_t h_dev_bytes = 0;
+};
+
+namespace {
+
+constexpr size_t kCounterBytes = 64;
+
+int ensure_ws(tdt_ctx *c, uint32_t n_msgs) {
+    const size_t need = kCounterBytes + 8ull * (n_msgs + 1);
+    if (need > c->ws_bytes) {
+        if (c->ws) HIPCHK(hipFree(c->ws));
+        c->ws = nullptr;
+        size_t cap = std::max<size_t>(need, c->ws_bytes * 2);
+        HIPCHK(hipMalloc(&c->ws, cap));
+        c->ws_bytes = cap;
+    }
+    return TDT_OK;
+}
+
+bool ws_supported(int ws) { return ws == 1 || ws == 2 || ws == 4 || ws == 8 || ws == 16; }
+
+bool policy_on(const tdt_ctx *c) {
+    // should_transform :192-200 (the size / tensor-shape terms are evaluated per message on
+    // the device)
+    return !(c->cpu.load() > c->cfg.cpu_usage_threshold) &&
+           c->bandwidth.load() < c->cfg.bandwidth_threshold_mbps;
+}
+
+template <int WS, int TEAM, int G, int MODE>
+int launch_encode_t(psy::EncodeArgs a, hipStream_t s) {
+    hipLaunchKernelGGL((psy::tdt_encode_kernel<WS, TEAM, G, MODE>), dim3(a.n_msgs), dim3(TEAM), 0, s, a);
+    return TDT_OK;
+}
+
+template <int WS, int MODE>
+int launch_encode_ws(psy::EncodeArgs a, bool small, hipStream_t s) {
+    if (small) return launch_encode_t<WS, 64, 4, MODE>(a, s);
+    return launch_encode_t<WS, 256, 16, MODE>(a, s);
+}
+
+template <int MODE>
+int launch_encode(tdt_ctx *c, psy::EncodeArgs a, hipStream_t s) {
+    const bool small = c->size_hint.load() <= 4096;
+    switch (c->cfg.word_size) {
+        case 1: return launch_encode_ws<1, MODE>(a, small, s);
+        case 2: return launch_encode_ws<2, MODE>(a, small, s);
+        case 4: return launch_encode_ws<4, MODE>(a, small, s);
+        case 8: return launch_encode_ws<8, MODE>(a, small, s);
+        case 16: return launch_encode_ws<16, MODE>(a, small, s);
+    }
+    return set_err(TDT_E_UNSUPPORTED, "word_size not supported on the GPU path");
+}
+
+int prep(tdt_ctx *c, uint32_t n_msgs, hipStream_t s) {
+    HIPCHK(hipSetDevice(c->device));
+    int st = ensure_ws(c, n_msgs);
+    if (st) return st;
+    HIPCHK(hipMemsetAsync(c->ws, 0, kCounterBytes + 8ull * n_msgs, s));
+    return TDT_OK;
+}
+
+int encode_common(tdt_ctx *c, int mode, const uint8_t *d_in, const uint64_t *d_in_off, uint32_t n_msgs,
+                  const int32_t *d_mapping, uint8_t *d_out, uint64_t out_cap, uint64_t *d_out_off,
+                  int32_t *d_status, uint32_t *d_hist, double *d_ent, int32_t *d_map, void *stream) {
+    if (!c) return set_err(TDT_E_ARG, "null context");
+    if (n_msgs == 0) return TDT_OK;
+    if (!d_in || !d_in_off) return set_err(TDT_E_ARG, "null input");
+    if (mode != psy::MODE_ANALYZE && (!d_out || !d_out_off)) return set_err(TDT_E_ARG, "null output");
+    if (mode == psy::MODE_MAPPED && !d_mapping) return set_err(TDT_E_ARG, "null mapping");
+    hipStream_t s = (hipStream_t)stream;
+    std::lock_guard<std::mutex> lk(c->mu);
+    int st = prep(c, n_msgs, s);
+    if (st) return st;
+    psy::EncodeArgs a{};
+    a.in = d_in;
+    a.in_off = d_in_off;
+    a.n_msgs = n_msgs;
+    a.out = d_out;
+    a.out_cap = out_cap;
+    a.out_off = d_out_off;
+    a.status = d_status;
+    a.mapping_in = d_mapping;
+    a.hist_out = d_hist;
+    a.ent_out = d_ent;
+    a.map_out = d_map;
+    a.ticket = reinterpret_cast<uint32_t *>(c->ws);
+    a.timeout = reinterpret_cast<uint32_t *>(c->ws) + 1;
+    a.lookback = reinterpret_cast<uint64_t *>(c->ws + kCounterBytes);
+    a.min_tensor = c->cfg.min_tensor_size;
+    a.policy_on = policy_on(c) ? 1 : 0;
+    if (mode == psy::MODE_ENCODE) st = launch_encode<psy::MODE_ENCODE>(c, a, s);
+    else if (mode == psy::MODE_MAPPED) st = launch_encode<psy::MODE_MAPPED>(c, a, s);
+    else st = launch_encode<psy::MODE_ANALYZE>(c, a, s);
+    if (st) return st;
+    HIPCHK(hipGetLastError());
+    return TDT_OK;
+}
+
+int decode_common(tdt_ctx *c, bool sizes_only, const uint8_t *d_in, const uint64_t *d_in_off, uint32_t n_msgs,
+                  uint8_t *d_out, uint64_t out_cap, uint64_t *d_out_off, uint64_t *d_sizes, int32_t *d_status,
+                  void *stream) {
+    if (!c) return set_err(TDT_E_ARG, "null context");
+    if (n_msgs == 0) return TDT_OK;
+    if (!d_in || !d_in_off) return set_err(TDT_E_ARG, "null input");
+    if (!sizes_only && (!d_out_off)) return set_err(TDT_E_ARG, "null output offsets");
+    if (sizes_only && !d_sizes) return set_err(TDT_E_ARG, "null sizes");
+    hipStream_t s = (hipStream_t)stream;
+    std::lock_guard<std::mutex> lk(c->mu);
+    int st = prep(c, n_msgs, s);
+    if (st) return st;
+    psy::DecodeArgs a{};
+    a.in = d_in;
+    a.in_off = d_in_off;
+    a.n_msgs = n_msgs;
+    a.out = d_out;
+    a.out_cap = out_cap;
+    a.out_off = d_out_off;
+    a.status = d_status;
+    a.sizes_out = d_sizes;
+    a.ticket = reinterpret_cast<uint32_t *>(c->ws);
+    a.timeout = reinterpret_cast<uint32_t *>(c->ws) + 1;
+    a.lookback = reinterpret_cast<uint64_t *>(c->ws + kCounterBytes);
+    const bool small = c->size_hint.load() <= 4096;
+    if (sizes_only) {
+        hipLaunchKernelGGL((psy::tdt_decode_kernel<64, 1>), dim3(n_msgs), dim3(64), 0, s, a);
+    } else if (small) {
+        hipLaunchKernelGGL((psy::tdt_decode_kernel<64, 0>), dim3(n_msgs), dim3(64), 0, s, a);
+    } else {
+        hipLaunchKernelGGL((psy::tdt_decode_kernel<256, 0>), dim3(n_msgs), dim3(256), 0, s, a);
+    }
+    HIPCHK(hipGetLastError());
+    return TDT_OK;
+}
+
+int ensure_host_dev(tdt_ctx *c, size_t bytes) {
+    if (bytes > c->h_dev_bytes) {
+        if (c->h_dev) HIPCHK(hipFree(c->h_dev));
+        c->h_dev = nullptr;
+        size_t cap = std::max(bytes, c->h_dev_bytes * 2);
+        HIPCHK(hipMalloc(&c->h_dev, cap));
+        c->h_dev_bytes = cap;
+    }
+    return TDT_OK;
+}
+
+size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+int host_path(tdt_ctx *c, bool encode, const uint8_t *h_in, const uint64_t *h_in_off, uint32_t n_msgs,
+              uint8_t *h_out, uint64_t out_cap, uint64_t *h_out_off, int32_t *h_status) {
+    if (!c) return set_err(TDT_E_ARG, "null context");
+    if (n_msgs == 0) {
+        if (h_out_off) h_out_off[0] = 0;
+        return TDT_OK;
+    }
+    HIPCHK(hipSetDevice(c->device));
+    const uint64_t in_bytes = h_in_off[n_msgs] - h_in_off[0];
+    const size_t o_in = 0;
+    const size_t o_off = align_up(o_in + in_bytes, 256);
+    const size_t o_out = align_up(o_off + 8ull * (n_msgs + 1), 256);
+    const size_t o_ooff = align_up(o_out + out_cap, 256);
+    const size_t o_st = align_up(o_ooff + 8ull * (n_msgs + 1), 256);
+    const size_t total = align_up(o_st + 4ull * n_msgs, 256);
+    int st;
+    {
+        std::lock_guard<std::mutex> lk(c->mu);
+        st = ensure_host_dev(c, total);
+    }
+    if (st) return st;
+    uint8_t *d = c->h_dev;
+    hipStream_t s = nullptr;
+    HIPCHK(hipMemcpyAsync(d + o_in, h_in + h_in_off[0], in_bytes, hipMemcpyHostToDevice, s));
+    // offsets rebased to 0
+    uint64_t *tmp = new uint64_t[n_msgs + 1];
+    for (uint32_t i = 0; i <= n_msgs; ++i) tmp[i] = h_in_off[i] - h_in_off[0];
+    hipError_t e = hipMemcpyAsync(d + o_off, tmp, 8ull * (n_msgs + 1), hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    delete[] tmp;
+    if (e != hipSuccess) return set_err(TDT_E_HIP, hipGetErrorString(e));
+    if (encode)
+        st = encode_common(c, psy::MODE_ENCODE, d + o_in, reinterpret_cast<uint64_t *>(d + o_off), n_msgs, nullptr,
+                           d + o_out, out_cap, reinterpret_cast<uint64_t *>(d + o_ooff),
+                           reinterpret_cast<int32_t *>(d + o_st), nullptr, nullptr, nullptr, s);
+    else
+        st = decode_common(c, false, d + o_in, reinterpret_cast<uint64_t *>(d + o_off), n_msgs, d + o_out, out_cap,
+                           reinterpret_cast<uint64_t *>(d + o_ooff), nullptr, reinterpret_cast<int32_t *>(d + o_st),
+                           s);
+    if (st) return st;
+    HIPCHK(hipMemcpyAsync(h_out_off, d + o_ooff, 8ull * (n_msgs + 1), hipMemcpyDeviceToHost, s));
+    if (h_status) HIPCHK(hipMemcpyAsync(h_status, d + o_st, 4ull * n_msgs, hipMemcpyDeviceToHost, s));
+    uint32_t timeout = 0;
+    HIPCHK(hipMemcpyAsync(&timeout, c->ws + 4, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (timeout) return set_err(TDT_E_HIP, "look-back timeout");
+    const uint64_t produced = std::min<uint64_t>(h_out_off[n_msgs], out_cap);
+    if (produced) HIPCHK(hipMemcpy(h_out, d + o_out, produced, hipMemcpyDeviceToHost));
+    return TDT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+void tdt_default_config(tdt_config *cfg) {
+    cfg->sample_fraction = 0.3f;
+    cfg->word_size = 4;
+    cfg->bandwidth_threshold_mbps = 100.0;
+    cfg->cpu_usage_threshold = 0.8;
+    cfg->min_tensor_size = 1024;
+}
+
+int tdt_ctx_create(int device, const tdt_config *cfg, tdt_ctx **out) {
+    if (!out) return set_err(TDT_E_ARG, "null out");
+    *out = nullptr;
+    tdt_config c;
+    if (cfg) c = *cfg;
+    else tdt_default_config(&c);
+    if (c.word_size <= 0) return set_err(TDT_E_CONFIG, "word_size must be positive");
+    if (!ws_supported(c.word_size)) return set_err(TDT_E_UNSUPPORTED, "GPU encoder supports word_size 1,2,4,8,16");
+    int ndev = 0;
+    HIPCHK(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) return set_err(TDT_E_ARG, "bad device");
+    tdt_ctx *x = new tdt_ctx();
+    x->device = device;
+    x->cfg = c;
+    *out = x;
+    return TDT_OK;
+}
+
+void tdt_ctx_destroy(tdt_ctx *ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->ws) (void)hipFree(ctx->ws);
+    if (ctx->h_dev) (void)hipFree(ctx->h_dev);
+    delete ctx;
+}
+
+void tdt_ctx_set_metrics(tdt_ctx *ctx, double bandwidth_mbps, double latency_ms, double cpu_usage) {
+    ctx->bandwidth.store(bandwidth_mbps);
+    ctx->latency.store(latency_ms);
+    ctx->cpu.store(cpu_usage);
+}
+
+void tdt_ctx_get_metrics(const tdt_ctx *ctx, double *bandwidth_mbps, double *latency_ms, double *cpu_usage) {
+    if (bandwidth_mbps) *bandwidth_mbps = ctx->bandwidth.load();
+    if (latency_ms) *latency_ms = ctx->latency.load();
+    if (cpu_usage) *cpu_usage = ctx->cpu.load();
+}
+
+void tdt_ctx_set_size_hint(tdt_ctx *ctx, uint64_t bytes) { ctx->size_hint.store(bytes); }
+
+int tdt_should_transform(const tdt_ctx *ctx, uint64_t n) {
+    if (n < ctx->cfg.min_tensor_size) return 0;
+    if (ctx->cpu.load() > ctx->cfg.cpu_usage_threshold) return 0;
+    if (!((n % 4 == 0) && (n >= 64))) return 0;
+    return ctx->bandwidth.load() < ctx->cfg.bandwidth_threshold_mbps ? 1 : 0;
+}
+
+uint64_t tdt_encode_bound(uint64_t n, int32_t word_size) {
+    const uint64_t w = word_size > 0 ? (uint64_t)word_size : 4;
+    const uint64_t tdt = 20 + 4 * w + 8 + 2 * n;
+    return std::max<uint64_t>(tdt, n + 4);
+}
+
+int tdt_encode_batch(tdt_ctx *ctx, const uint8_t *d_in, const uint64_t *d_in_off, uint32_t n_msgs, uint8_t *d_out,
+                     uint64_t out_cap, uint64_t *d_out_off, int32_t *d_status, void *stream) {
+    return encode_common(ctx, psy::MODE_ENCODE, d_in, d_in_off, n_msgs, nullptr, d_out, out_cap, d_out_off, d_status,
+                         nullptr, nullptr, nullptr, stream);
+}
+
+int tdt_encode_with_mapping_batch(tdt_ctx *ctx, const uint8_t *d_in, const uint64_t *d_in_off, uint32_t n_msgs,
+                                  const int32_t *d_mapping, uint8_t *d_out, uint64_t out_cap, uint64_t *d_out_off,
+                                  int32_t *d_status, void *stream) {
+    return encode_common(ctx, psy::MODE_MAPPED, d_in, d_in_off, n_msgs, d_mapping, d_out, out_cap, d_out_off,
+                         d_status, nullptr, nullptr, nullptr, stream);
+}
+
+int tdt_analyze_batch(tdt_ctx *ctx, const uint8_t *d_in, const uint64_t *d_in_off, uint32_t n_msgs, uint32_t *d_hist,
+                      double *d_entropy, int32_t *d_mapping, int32_t *d_status, void *stream) {
+    return encode_common(ctx, psy::MODE_ANALYZE, d_in, d_in_off, n_msgs, nullptr, nullptr, 0, nullptr, d_status,
+                         d_hist, d_entropy, d_mapping, stream);
+}
+
+int tdt_decode_batch(tdt_ctx *ctx, const uint8_t *d_in, const uint64_t *d_in_off, uint32_t n_msgs, uint8_t *d_out,
+                     uint64_t out_cap, uint64_t *d_out_off, int32_t *d_status, void *stream) {
+    return decode_common(ctx, false, d_in, d_in_off, n_msgs, d_out, out_cap, d_out_off, nullptr, d_status, stream);
+}
+
+int tdt_decoded_sizes_batch(tdt_ctx *ctx, const uint8_t *d_in, const uint64_t *d_in_off, uint32_t n_msgs,
+                            uint64_t *d_sizes, int32_t *d_status, void *stream) {
+    return decode_common(ctx, true, d_in, d_in_off, n_msgs, nullptr, 0, nullptr, d_sizes, d_status, stream);
+}
+
+int tdt_encode_host(tdt_ctx *ctx, const uint8_t *h_in, const uint64_t *h_in_off, uint32_t n_msgs, uint8_t *h_out,
+                    uint64_t out_cap, uint64_t *h_out_off, int32_t *h_status) {
+    return host_path(ctx, true, h_in, h_in_off, n_msgs, h_out, out_cap, h_out_off, h_status);
+}
+
+int tdt_decode_host(tdt_ctx *ctx, const uint8_t *h_in, const uint64_t *h_in_off, uint32_t n_msgs, uint8_t *h_out,
+                    uint64_t out_cap, uint64_t *h_out_off, int32_t *h_status) {
+    return host_path(ctx, false, h_in, h_in_off, n_msgs, h_out, out_cap, h_out_off, h_status);
+}
+
+const char *tdt_last_error(void) { return g_err.c_str(); }
+
+const char *tdt_status_string(int status) {
+    switch (status) {
+        case TDT_OK: return "OK";
+        case TDT_E_SHORT: return "TDT: Invalid encoded data size";
+        case TDT_E_MAGIC: return "Invalid TDT magic number";
+        case TDT_E_TRUNCATED: return "TDT: truncated blob";
+        case TDT_E_BAD_MAPPING: return "TDT: invalid cluster mapping";
+        case TDT_E_CAPACITY: return "TDT: output capacity exceeded";
+        case TDT_E_UNSUPPORTED: return "TDT: word size not supported on the GPU path";
+        case TDT_E_BAD_HEADER: return "TDT: word size 0";
+        case TDT_E_CONFIG: return "TDT: invalid configuration";
+        case TDT_E_HIP: return "TDT: HIP runtime error";
+        case TDT_E_ARG: return "TDT: invalid argument";
+    }
+    return "TDT: unknown status";
+}
+
+}  // extern "C"

@@ -1,0 +1,254 @@
+// tdt_device.h — CDNA4 device building blocks shared by the TDT encode/decode kernels.
+//
+//   * wave64 inclusive scans on DPP (row_shr 1/2/4/8 + row_bcast 15/31: 12 VALU, no LDS)
+//   * team (workgroup) exclusive scans: one DPP wave scan + one LDS exchange + one barrier
+//   * decoupled look-back over message ids (single-pass compaction of variable-length
+//     outputs; the status word carries the value, so no separate flag/fence is needed:
+//     MI355X_MICROARCH.md "R2: the data IS the flag", 8-byte relaxed agent-scope atomics)
+//   * byte-exact global loads/stores that never touch bytes outside the buffer
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace psy {
+
+constexpr int kWave = 64;
+
+__device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
+
+template <int CTRL, int ROWMASK = 0xf, int BANKMASK = 0xf>
+__device__ __forceinline__ uint32_t dpp_mov(uint32_t x) {
+    // Lanes whose source is outside the row / disabled by ROWMASK receive 0 (the identity
+    // of both scan operators used here).
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROWMASK, BANKMASK, false);
+}
+
+struct OpAdd {
+    __device__ __forceinline__ static uint32_t f(uint32_t a, uint32_t b) { return a + b; }
+};
+struct OpMax {
+    __device__ __forceinline__ static uint32_t f(uint32_t a, uint32_t b) { return a > b ? a : b; }
+};
+
+// Inclusive wave64 scan with identity 0.
+template <class Op>
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+    x = Op::f(x, dpp_mov<0x111>(x));       // row_shr:1
+    x = Op::f(x, dpp_mov<0x112>(x));       // row_shr:2
+    x = Op::f(x, dpp_mov<0x114>(x));       // row_shr:4
+    x = Op::f(x, dpp_mov<0x118>(x));       // row_shr:8
+    x = Op::f(x, dpp_mov<0x142, 0xa>(x));  // row_bcast:15 into rows 1,3
+    x = Op::f(x, dpp_mov<0x143, 0xc>(x));  // row_bcast:31 into rows 2,3
+    return x;
+}
+
+__device__ __forceinline__ uint32_t wave_shift_up1(uint32_t x) {
+    // lane l receives lane l-1's value, lane 0 receives 0
+    return (uint32_t)__shfl_up((int)x, 1) * (lane_id() != 0);
+}
+
+template <class Op>
+__device__ __forceinline__ uint32_t wave_reduce(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan<Op>(x), 63);
+}
+
+// Team-wide exclusive scan of NV values per thread in threadIdx order.
+// slots: LDS scratch of W*NV uint32 (callers alternate two slot buffers between
+// consecutive scans so that only ONE barrier per scan is needed).
+// On return v[k] holds the exclusive prefix and tot[k] the team total (uniform).
+template <int W, int NV, class Op>
+__device__ __forceinline__ void team_excl_scan(uint32_t (&v)[NV], uint32_t (&tot)[NV], uint32_t *slots) {
+    const int lane = lane_id();
+    uint32_t inc[NV];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) inc[k] = wave_incl_scan<Op>(v[k]);
+    if constexpr (W == 1) {
+#pragma unroll
+        for (int k = 0; k < NV; ++k) {
+            tot[k] = (uint32_t)__builtin_amdgcn_readlane((int)inc[k], 63);
+            v[k] = wave_shift_up1(inc[k]);
+        }
+    } else {
+        const int w = threadIdx.x >> 6;
+        if (lane == 63) {
+#pragma unroll
+            for (int k = 0; k < NV; ++k) slots[w * NV + k] = inc[k];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < NV; ++k) {
+            uint32_t pre = 0, t = 0;
+#pragma unroll
+            for (int ww = 0; ww < W; ++ww) {
+                uint32_t s = slots[ww * NV + k];
+                if (ww < w) pre = Op::f(pre, s);
+                t = Op::f(t, s);
+            }
+            tot[k] = t;
+            v[k] = Op::f(pre, wave_shift_up1(inc[k]));
+        }
+    }
+}
+
+template <int W>
+__device__ __forceinline__ void team_sync() {
+    if constexpr (W == 1) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    } else {
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// Decoupled look-back over message ids.  st[i] = flag(2 bits) | value(62 bits);
+// flag 1 = aggregate (this message's size) published, 2 = inclusive prefix published.
+// Message ids are claimed through an atomic ticket in launch order, so every predecessor
+// is already resident and publishes its aggregate without waiting: no deadlock, whatever
+// the dispatch order.  The spin is bounded; on timeout *timeout is set and 0 is assumed.
+constexpr uint64_t kLbAgg = 1ull << 62;
+constexpr uint64_t kLbInc = 2ull << 62;
+constexpr uint64_t kLbVal = (1ull << 62) - 1;
+
+__device__ __forceinline__ void lb_store(uint64_t *p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t lb_load(uint64_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Called by ONE thread.  Returns the exclusive prefix of message i.
+__device__ __forceinline__ uint64_t lookback_excl(uint64_t *st, uint32_t i, uint64_t agg,
+                                                  uint32_t *timeout) {
+    if (i == 0) {
+        lb_store(&st[0], kLbInc | agg);
+        return 0;
+    }
+    lb_store(&st[i], kLbAgg | agg);
+    uint64_t excl = 0;
+    int64_t j = (int64_t)i - 1;
+    uint32_t spins = 0;
+    while (j >= 0) {
+        uint64_t s = lb_load(&st[j]);
+        uint64_t f = s >> 62;
+        if (f == 0) {
+            if (++spins > (1u << 26)) {
+                atomicOr(timeout, 1u);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        excl += s & kLbVal;
+        if (f == 2) break;
+        --j;
+    }
+    lb_store(&st[i], kLbInc | (excl + agg));
+    return excl;
+}
+
+// ---------------------------------------------------------------------------------------
+// Byte-exact accesses.
+__device__ __forceinline__ uint32_t ld_u8(const uint8_t *p) { return *p; }
+
+__device__ __forceinline__ uint32_t ld_u32_bytes(const uint8_t *p) {
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+// 16 bytes from p, any alignment; bytes at index >= valid read as 0 and are not touched.
+__device__ __forceinline__ uint4 ld16_any(const uint8_t *p, int valid) {
+    uint4 r;
+    const uintptr_t a = (uintptr_t)p;
+    if (valid >= 16 && (a & 15) == 0) {
+        r = *reinterpret_cast<const uint4 *>(p);
+    } else if (valid >= 16 && (a & 3) == 0) {
+        const uint32_t *q = reinterpret_cast<const uint32_t *>(p);
+        r.x = q[0];
+        r.y = q[1];
+        r.z = q[2];
+        r.w = q[3];
+    } else {
+        uint32_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+            if (i < valid) w[i >> 2] |= (uint32_t)p[i] << (8 * (i & 3));
+        r.x = w[0];
+        r.y = w[1];
+        r.z = w[2];
+        r.w = w[3];
+    }
+    return r;
+}
+
+// Store the first `valid` bytes of v at p (any alignment).
+__device__ __forceinline__ void st16_any(uint8_t *p, uint4 v, int valid) {
+    const uintptr_t a = (uintptr_t)p;
+    if (valid >= 16 && (a & 15) == 0) {
+        *reinterpret_cast<uint4 *>(p) = v;
+    } else if (valid >= 16 && (a & 3) == 0) {
+        uint32_t *q = reinterpret_cast<uint32_t *>(p);
+        q[0] = v.x;
+        q[1] = v.y;
+        q[2] = v.z;
+        q[3] = v.w;
+    } else {
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+            if (i < valid) p[i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+    }
+}
+
+// Team copy global -> global, arbitrary alignment and length.
+template <int TEAM>
+__device__ __forceinline__ void team_copy_g2g(uint8_t *dst, const uint8_t *src, uint64_t len) {
+    const int tid = threadIdx.x;
+    const uintptr_t d = (uintptr_t)dst, s = (uintptr_t)src;
+    if (((d ^ s) & 15) == 0) {
+        uint64_t head = ((16 - (d & 15)) & 15);
+        if (head > len) head = len;
+        if ((uint64_t)tid < head) dst[tid] = src[tid];
+        const uint64_t body = (len - head) & ~(uint64_t)15;
+        const uint4 *sv = reinterpret_cast<const uint4 *>(src + head);
+        uint4 *dv = reinterpret_cast<uint4 *>(dst + head);
+        for (uint64_t k = tid; k < body / 16; k += TEAM) dv[k] = sv[k];
+        for (uint64_t k = head + body + tid; k < len; k += TEAM) dst[k] = src[k];
+    } else if (((d ^ s) & 3) == 0) {
+        uint64_t head = ((4 - (d & 3)) & 3);
+        if (head > len) head = len;
+        if ((uint64_t)tid < head) dst[tid] = src[tid];
+        const uint64_t body = (len - head) & ~(uint64_t)3;
+        const uint32_t *sv = reinterpret_cast<const uint32_t *>(src + head);
+        uint32_t *dv = reinterpret_cast<uint32_t *>(dst + head);
+        for (uint64_t k = tid; k < body / 4; k += TEAM) dv[k] = sv[k];
+        for (uint64_t k = head + body + tid; k < len; k += TEAM) dst[k] = src[k];
+    } else {
+        for (uint64_t k = tid; k < len; k += TEAM) dst[k] = src[k];
+    }
+}
+
+// Team fill of zeros, arbitrary alignment.
+template <int TEAM>
+__device__ __forceinline__ void team_zero(uint8_t *dst, uint64_t len) {
+    const int tid = threadIdx.x;
+    const uintptr_t d = (uintptr_t)dst;
+    uint64_t head = ((16 - (d & 15)) & 15);
+    if (head > len) head = len;
+    if ((uint64_t)tid < head) dst[tid] = 0;
+    const uint64_t body = (len - head) & ~(uint64_t)15;
+    uint4 *dv = reinterpret_cast<uint4 *>(dst + head);
+    for (uint64_t k = tid; k < body / 16; k += TEAM) dv[k] = make_uint4(0, 0, 0, 0);
+    for (uint64_t k = head + body + tid; k < len; k += TEAM) dst[k] = 0;
+}
+
+// Bytes 0..3 of x that differ from the byte before them (prev-byte chain across dwords
+// given by `below`, whose top byte precedes byte 0 of x), as a 4-bit mask.
+__device__ __forceinline__ uint32_t neq_prev_mask4(uint32_t x, uint32_t below) {
+    const uint32_t t = __builtin_amdgcn_alignbyte(x, below, 3);  // byte k = byte k-1 of {x:below}
+    const uint32_t d = x ^ t;
+    const uint32_t nz = (((d & 0x7f7f7f7fu) + 0x7f7f7f7fu) | d) & 0x80808080u;
+    return (((nz >> 7) * 0x00204081u) >> 21) & 0xfu;  // gather bits 0,8,16,24 into bits 0..3
+}
+
+}  // namespace psy

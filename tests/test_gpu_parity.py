@@ -1,0 +1,343 @@
+"""GPU parity: the HIP codec (through the C ABI) against the golden vectors made by the
+reference codec, and against the CPU oracle on seeded inputs.  Bit-exact everywhere: this
+is byte/integer work (the only floating point, the entropy decision, is restated
+bit-exactly; tests/test_log2_restatement.py)."""
+import numpy as np
+import pytest
+
+from oracle.oracle import Oracle
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+E_CAPACITY, E_UNSUPPORTED = 5, 6
+
+
+@pytest.fixture(scope="module")
+def orc():
+    return Oracle()
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    from psyne_amd import _lib
+    _lib.load()  # the HIP library must be the thing under test
+
+
+def make_codec(ws=4, min_tensor=1024, bw=10.0, cpu=0.5, hint=None):
+    from psyne_amd import TDTConfig, TdtCodec
+    c = TdtCodec(TDTConfig(sample_fraction=1.0, word_size=ws, min_tensor_size=min_tensor))
+    c.set_metrics(bw, 1.0, cpu)
+    if hint is not None:
+        c.set_size_hint(hint)
+    return c
+
+
+def pack(msgs, lead=0, align=1):
+    """Concatenate messages (optionally misaligned by `lead` bytes) → device tensors."""
+    sizes = [len(m) for m in msgs]
+    off = np.zeros(len(msgs) + 1, np.int64)
+    pos = lead
+    for i, s in enumerate(sizes):
+        off[i] = pos
+        pos += s
+        if align > 1:
+            pos = (pos + align - 1) // align * align
+    off[-1] = pos
+    buf = np.zeros(max(pos, 1), np.uint8)
+    for i, m in enumerate(msgs):
+        buf[off[i]:off[i] + len(m)] = np.frombuffer(bytes(m), np.uint8) if not isinstance(m, np.ndarray) else m
+    # with align>1 the gaps belong to the preceding message; rebuild exact offsets
+    if align > 1:
+        exact = []
+        for i, m in enumerate(msgs):
+            exact.append((off[i], off[i] + len(m)))
+        return buf, exact
+    return buf, off
+
+
+def encode_list(codec, msgs, lead=0):
+    buf, off = pack(msgs, lead)
+    # offsets are absolute into buf; the message list starts at `lead`
+    d = torch.from_numpy(buf).cuda()
+    o = torch.from_numpy(off).cuda()
+    enc, eoff, st = codec.encode_batch(d, o)
+    torch.cuda.synchronize()
+    e, eo, s = enc.cpu().numpy(), eoff.cpu().numpy(), st.cpu().numpy()[: len(msgs)]
+    return [e[eo[i]:eo[i + 1]].tobytes() for i in range(len(msgs))], s, eo
+
+
+def decode_list(codec, blobs, cap=None):
+    buf, off = pack(blobs)
+    d = torch.from_numpy(buf).cuda()
+    o = torch.from_numpy(off).cuda()
+    if cap is None:
+        out, doff, st = codec.decode_batch(d, o)
+    else:
+        out = torch.empty(max(cap, 1), dtype=torch.uint8, device="cuda")
+        out, doff, st = codec.decode_batch(d, o, out=out)
+    torch.cuda.synchronize()
+    x, xo, s = out.cpu().numpy(), doff.cpu().numpy(), st.cpu().numpy()[: len(blobs)]
+    return [x[xo[i]:xo[i + 1]].tobytes() for i in range(len(blobs))], s
+
+
+def grad(rng, nfloat):
+    x = rng.normal(0, 0.01, nfloat).astype(np.float32)
+    x[rng.random(nfloat) < 0.7] = 0
+    return x.view(np.uint8)
+
+
+# ----------------------------------------------------------------------------- golden
+def _encode_groups(golden, op):
+    groups = {}
+    for c in golden:
+        if c.op == op:
+            groups.setdefault((c.ws, c.bandwidth, c.cpu, c.min_tensor), []).append(c)
+    return groups
+
+
+@pytest.mark.parametrize("hint", [1024, 65536])
+def test_golden_encode(golden, hint):
+    n = 0
+    for (ws, bw, cpu, mt), cases in _encode_groups(golden, "encode").items():
+        codec = make_codec(ws, mt, bw, cpu, hint)
+        got, st, _ = encode_list(codec, [c.input for c in cases])
+        for c, g, s in zip(cases, got, st):
+            assert s == 0, (c.name, s)
+            assert g == c.expected.tobytes(), c.name
+            n += 1
+    assert n > 100
+
+
+def test_golden_encode_with_mapping(golden):
+    cases = [c for c in golden if c.op == "encode_with_mapping"]
+    codec = make_codec(4)
+    buf, off = pack([c.input for c in cases])
+    mp = torch.tensor(np.array([c.mapping for c in cases], np.int32).reshape(-1)).cuda()
+    enc, eoff, st = codec.encode_batch(torch.from_numpy(buf).cuda(), torch.from_numpy(off).cuda(), mapping=mp)
+    torch.cuda.synchronize()
+    e, eo = enc.cpu().numpy(), eoff.cpu().numpy()
+    for i, c in enumerate(cases):
+        assert int(st[i]) == 0
+        assert e[eo[i]:eo[i + 1]].tobytes() == c.expected.tobytes(), c.name
+
+
+@pytest.mark.parametrize("hint", [1024, 65536])
+def test_golden_decode(golden, hint):
+    codec = make_codec(4, hint=hint)
+    blobs, want = [], []
+    for c in golden:
+        if c.op in ("encode", "encode_with_mapping"):
+            blobs.append(c.expected.tobytes())
+            want.append((0, c.input.tobytes(), c.name))
+        elif c.op == "decode":
+            blobs.append(c.input.tobytes())
+            want.append((c.status, c.expected.tobytes() if c.status == 0 else b"", c.name))
+    got, st = decode_list(codec, blobs)
+    for (ws_, exp, name), g, s in zip(want, got, st):
+        assert s == ws_, (name, s, ws_)
+        if s == 0:
+            assert g == exp, name
+
+
+def test_golden_policy(golden):
+    for c in golden:
+        if c.op != "policy":
+            continue
+        codec = make_codec(c.ws, c.min_tensor, c.bandwidth, c.cpu)
+        assert codec.should_transform(c.n) == c.expect, c.name
+
+
+# ------------------------------------------------------------------------- vs oracle
+def check_vs_oracle(orc, codec, msgs, ws=4, lead=0, bw=10.0, cpu=0.5, mt=1024):
+    got, st, eo = encode_list(codec, msgs, lead)
+    cfg = orc.config(word_size=ws, min_tensor_size=mt)
+    blobs = []
+    for i, m in enumerate(msgs):
+        want = orc.encode(m, cfg=cfg, bandwidth=bw, cpu=cpu)
+        assert st[i] == 0
+        assert got[i] == want, f"message {i} (n={len(m)})"
+        blobs.append(want)
+    dec, dst = decode_list(codec, blobs)
+    for i, m in enumerate(msgs):
+        assert dst[i] == 0 and dec[i] == bytes(m), f"decode {i}"
+    return got
+
+
+@pytest.mark.parametrize("hint", [1024, 65536])
+def test_uniform_1k(orc, hint):
+    rng = np.random.default_rng(11)
+    msgs = [rng.integers(0, 256, 1024, dtype=np.uint8) for _ in range(512)]
+    check_vs_oracle(orc, make_codec(hint=hint), msgs)
+
+
+def test_gradient_64k(orc):
+    rng = np.random.default_rng(12)
+    msgs = [grad(rng, 16384) for _ in range(24)]
+    check_vs_oracle(orc, make_codec(), msgs)
+
+
+@pytest.mark.parametrize("hint", [1024, 65536])
+def test_large_streaming_path(orc, hint):
+    # > 64 KiB (resident limit) → the non-resident streaming rounds
+    rng = np.random.default_rng(13)
+    msgs = [grad(rng, 262144), rng.integers(0, 256, 200000, dtype=np.uint8), grad(rng, 70000)]
+    check_vs_oracle(orc, make_codec(hint=hint), msgs)
+
+
+def test_zipf_mix(orc):
+    rng = np.random.default_rng(14)
+    r = np.minimum(rng.zipf(1.5, 300), 1024)
+    msgs = []
+    for i, k in enumerate(r):
+        n = int(64 * k)
+        msgs.append(grad(rng, n // 4) if i % 2 else rng.integers(0, 256, n, dtype=np.uint8))
+    msgs += [rng.integers(0, 256, n, dtype=np.uint8) for n in (0, 1, 3, 63, 64, 1022, 1026, 1027, 1028)]
+    check_vs_oracle(orc, make_codec(), msgs)
+
+
+@pytest.mark.parametrize("lead", [1, 2, 3, 4, 8, 12])
+def test_misaligned_inputs(orc, lead):
+    rng = np.random.default_rng(15 + lead)
+    msgs = [rng.integers(0, 4, int(n), dtype=np.uint8) for n in rng.integers(256, 3000, 40) * 4]
+    msgs += [grad(rng, 4099), rng.integers(0, 256, 1030, dtype=np.uint8)]
+    check_vs_oracle(orc, make_codec(), msgs, lead=lead)
+
+
+def test_rle_cap_boundaries(orc):
+    """Runs around the 255 cap at every phase relative to the 16-byte groups."""
+    rng = np.random.default_rng(16)
+    msgs = [np.zeros(65536, np.uint8), np.full(65536, 7, np.uint8)]
+    for L in (254, 255, 256, 509, 510, 511, 765, 766, 1020, 4000):
+        for phase in (0, 1, 5, 15):
+            v = rng.integers(0, 256, 2048, dtype=np.uint8)
+            v[100 + phase:100 + phase + L] = 0x55
+            msgs.append(v)
+    # stream-position runs that cross many groups in one stream only
+    w = np.zeros((8192, 4), np.uint8)
+    w[:, 0] = rng.integers(0, 256, 8192)
+    msgs.append(w.reshape(-1))
+    w2 = np.zeros((8192, 4), np.uint8)
+    w2[:, 3] = rng.integers(0, 2, 8192)
+    msgs.append(w2.reshape(-1))
+    check_vs_oracle(orc, make_codec(), msgs)
+    check_vs_oracle(orc, make_codec(hint=1024), msgs)
+
+
+@pytest.mark.parametrize("ws", [1, 2, 8, 16])
+def test_word_sizes(orc, ws):
+    rng = np.random.default_rng(17 + ws)
+    msgs = [grad(rng, 1024 * (i + 1)) if i % 2 else rng.integers(0, 256, 2048 * (i + 1), dtype=np.uint8)
+            for i in range(6)]
+    msgs += [rng.integers(0, 3, 4096, dtype=np.uint8), np.zeros(4096, np.uint8)]
+    msgs += [rng.integers(0, 256, 1028, dtype=np.uint8)]  # 1028 % 8 != 0 → UNCP for ws 8/16
+    check_vs_oracle(orc, make_codec(ws=ws), msgs, ws=ws)
+
+
+def test_policy_passthrough(orc):
+    rng = np.random.default_rng(18)
+    msgs = [rng.integers(0, 256, 4096, dtype=np.uint8) for _ in range(8)]
+    for bw, cpu in ((100.0, 0.5), (1000.0, 0.3), (25.0, 0.9)):
+        got, st, _ = encode_list(make_codec(bw=bw, cpu=cpu), msgs)
+        for g, m in zip(got, msgs):
+            assert g == b"PCNU" + m.tobytes()
+
+
+def test_empty_and_tiny(orc):
+    codec = make_codec(min_tensor=0)
+    msgs = [np.zeros(0, np.uint8), np.arange(4, dtype=np.uint8), np.arange(64, dtype=np.uint8),
+            np.zeros(64, np.uint8), np.arange(68, dtype=np.uint8)]
+    check_vs_oracle(orc, codec, msgs, mt=0)
+
+
+def test_capacity_error():
+    rng = np.random.default_rng(19)
+    msgs = [rng.integers(0, 256, 4096, dtype=np.uint8) for _ in range(16)]
+    codec = make_codec()
+    buf, off = pack(msgs)
+    out = torch.empty(20000, dtype=torch.uint8, device="cuda")
+    _, eoff, st = codec.encode_batch(torch.from_numpy(buf).cuda(), torch.from_numpy(off).cuda(), out=out)
+    torch.cuda.synchronize()
+    st = st.cpu().numpy()
+    eo = eoff.cpu().numpy()
+    assert st[0] == 0 and st[-1] == E_CAPACITY
+    # offsets still describe the full (unwritten) layout
+    assert np.all(np.diff(eo) > 0)
+
+
+def test_analyze(orc):
+    rng = np.random.default_rng(20)
+    msgs = [grad(rng, 16384), rng.integers(0, 256, 1024, dtype=np.uint8), np.zeros(2048, np.uint8)]
+    codec = make_codec()
+    buf, off = pack(msgs)
+    hist, ent, mp, st = codec.analyze_batch(torch.from_numpy(buf).cuda(), torch.from_numpy(off).cuda())
+    for i, m in enumerate(msgs):
+        h, e, p = orc.analyze(m)
+        assert np.array_equal(hist[i].cpu().numpy().astype(np.uint32), h)
+        assert ent[i].cpu().numpy().tobytes() == e.tobytes()  # bit-exact doubles
+        assert np.array_equal(mp[i].cpu().numpy(), p)
+
+
+def test_roundtrip_many_64k():
+    """Size-independent properties at scale: round trip, offsets = prefix of blob sizes."""
+    rng = np.random.default_rng(21)
+    n = 2048
+    x = torch.empty(n * 16384, dtype=torch.float32, device="cuda").normal_(0, 0.01)
+    x[torch.rand(n * 16384, device="cuda") < 0.7] = 0
+    d = x.view(torch.uint8)
+    o = torch.arange(n + 1, dtype=torch.int64, device="cuda") * 65536
+    codec = make_codec()
+    enc, eoff, st = codec.encode_batch(d, o)
+    dec, doff, dst = codec.decode_batch(enc, eoff)
+    torch.cuda.synchronize()
+    assert int(st[:n].abs().sum()) == 0 and int(dst[:n].abs().sum()) == 0
+    assert torch.equal(dec[: n * 65536], d)
+    assert torch.equal(doff, o)
+    eo = eoff.cpu().numpy()
+    e = enc.cpu().numpy()
+    orc = Oracle()
+    for i in rng.integers(0, n, 16):
+        want = orc.encode(d[i * 65536:(i + 1) * 65536].cpu().numpy(), cfg=orc.config(), bandwidth=10.0)
+        assert e[eo[i]:eo[i + 1]].tobytes() == want
+
+
+def test_many_tiny_lookback():
+    # 200k UNCP messages: exercises the look-back chain at depth
+    rng = np.random.default_rng(22)
+    sizes = rng.integers(0, 40, 200000)
+    data = rng.integers(0, 256, int(sizes.sum()), dtype=np.uint8)
+    off = np.zeros(sizes.size + 1, np.int64)
+    off[1:] = np.cumsum(sizes)
+    codec = make_codec(hint=64)
+    enc, eoff, st = codec.encode_batch(torch.from_numpy(data).cuda(), torch.from_numpy(off).cuda())
+    torch.cuda.synchronize()
+    eo = eoff.cpu().numpy()
+    assert np.array_equal(np.diff(eo), sizes + 4)
+    e = enc.cpu().numpy()
+    i = 12345
+    assert e[eo[i]:eo[i + 1]].tobytes() == b"PCNU" + data[off[i]:off[i + 1]].tobytes()
+
+
+def test_protocol_mirror():
+    from psyne_amd import TDTCompressionProtocol, TDTConfig
+    p = TDTCompressionProtocol(TDTConfig(sample_fraction=1.0))
+    rng = np.random.default_rng(23)
+    m = grad(rng, 4096).tobytes()
+    assert p.protocol_name() == "TDT-Compression" and p.is_lossless()
+    blob = p.encode(m)
+    assert blob[:4] == b"PCNU"  # default bandwidth 100 Mbps → passthrough (:200, :352)
+    p.update_network_metrics(10.0, 1.0)
+    assert p.should_transform(m, len(m))
+    blob = p.encode(m)
+    assert blob[:4] == b"DTDT" and p.decode(blob) == m
+    assert p.transformation_ratio() > 1.0
+    orc = Oracle()
+    assert blob == orc.encode(np.frombuffer(m, np.uint8), cfg=orc.config(), bandwidth=10.0)
+    with pytest.raises(RuntimeError, match="TDT: Invalid encoded data size"):
+        p.decode(b"ab")
+    with pytest.raises(RuntimeError, match="Invalid TDT magic number"):
+        p.decode(b"XXXXYYYYZZZZ")
+    p.analyze_data(m, len(m))
+    _, e, _ = orc.analyze(np.frombuffer(m, np.uint8))
+    assert p.get_average_entropy() == sum(float(v) for v in e) / 4
