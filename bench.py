@@ -1,0 +1,274 @@
+#!/usr/bin/env python3
+"""TDT encode+decode throughput on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[2] = SURVEY.md §8(d) C3): per GPU, 262,144 messages of
+64 KiB float32 "gradient-like" payload (70 % exact 0.0f, else N(0, 0.01) — the
+GRADIENTS generator of the reference's tdt_compression_benchmark.cpp:52-66), generated on
+the device with a fixed seed.  One STEP = tdt_encode_batch over the whole batch (compacted
+blobs + offsets) followed by tdt_decode_batch of those blobs (compacted payloads), inputs
+already resident in HBM.  Compression is on (bandwidth 10 Mbps < 100 Mbps threshold) and the
+mapping is computed from every word (the reference's sample_fraction = 1.0, deterministic).
+
+value = payload bytes round-tripped by all ranks / max-over-ranks wall time, in GiB/s.
+Multi-GPU: messages are independent, so each rank owns its own batch (weak scaling, no
+collective on the data path; the only collectives are the timing barriers/all-reduce).
+
+Extra fields: roofline (dominant kernel, HIP events on the launch stream), cpu_baseline
+(the reference codec compiled where it lies, timed on this host), ratio and per-kernel ms.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import pathlib
+import sys
+import time
+
+ROOT = pathlib.Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--msgs", type=int, default=262144)
+    ap.add_argument("--msg-bytes", type=int, default=65536)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline duration (0 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = all usable host cores")
+    ap.add_argument("--host-inclusive", action="store_true", help="also time pinned H2D+kernel+D2H")
+    ap.add_argument("--seed", type=int, default=0x5EED0002)
+    return ap.parse_args()
+
+
+def gen_gradient(torch, n_msgs, msg_bytes, seed, device):
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    nf = n_msgs * msg_bytes // 4
+    x = torch.empty(nf, dtype=torch.float32, device=device)
+    chunk = 1 << 28
+    for s in range(0, nf, chunk):
+        e = min(nf, s + chunk)
+        v = torch.empty(e - s, dtype=torch.float32, device=device).normal_(0.0, 0.01, generator=g)
+        m = torch.rand(e - s, device=device, generator=g) < 0.7
+        v.masked_fill_(m, 0.0)
+        x[s:e] = v
+        del v, m
+    return x.view(torch.uint8)
+
+
+def load_traffic(config_key):
+    """HBM bytes per launch measured with rocprofv3 PMC passes (profiles/*_traffic.json)."""
+    best = None
+    for p in sorted((ROOT / "profiles").glob("*_traffic.json")):
+        try:
+            d = json.loads(p.read_text())
+        except Exception:
+            continue
+        if d.get("config") == config_key:
+            best = d
+    return best
+
+
+def cpu_baseline(data_u8, msg_bytes, target_s, threads):
+    """Time the REFERENCE codec (oracle/_ref, compiled from the reference header) on a
+    bounded sample of the same messages; fall back to the C restatement if absent."""
+    import numpy as np
+    from oracle.oracle import Reference, Oracle
+    n_sample = 512
+    sample = data_u8[: n_sample * msg_bytes].cpu().numpy()
+    off = np.arange(n_sample + 1, dtype=np.uint64) * msg_bytes
+    if Reference.available():
+        ref = Reference()
+        # calibrate on 1 thread, then scale reps to ~target_s on `threads` threads
+        t1, _ = ref.bench(sample[: 32 * msg_bytes], off[:33], sample_fraction=0.3, threads=1, reps=1)
+        per_msg = t1 / 32
+        reps = max(1, int(target_s * threads / (per_msg * n_sample)))
+        secs, enc = ref.bench(sample, off, sample_fraction=0.3, threads=threads, reps=reps)
+        payload = n_sample * msg_bytes * reps
+        return dict(value=payload / secs / 2**30, unit="GiB/s", cores=threads, kind="reference",
+                    sample="%d x %d B messages x %d reps, reference TDTCompressionProtocol (default "
+                           "TDTConfig, sample_fraction 0.3), encode+decode, one object per thread, %.1f s"
+                           % (n_sample, msg_bytes, reps, secs),
+                    ratio=float(payload / enc))
+    orc = Oracle()
+    t0 = time.perf_counter()
+    reps = 0
+    while time.perf_counter() - t0 < target_s:
+        for i in range(n_sample):
+            b = orc.encode(sample[off[i]:off[i + 1]], bandwidth=10.0)
+            orc.decode(b)
+        reps += 1
+    secs = time.perf_counter() - t0
+    return dict(value=n_sample * msg_bytes * reps / secs / 2**30, unit="GiB/s", cores=1, kind="port",
+                sample="%d x %d B messages x %d reps, oracle restatement, 1 thread" % (n_sample, msg_bytes, reps))
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from psyne_amd import TDTConfig, TdtCodec
+
+    n, mb = a.msgs, a.msg_bytes
+    data = gen_gradient(torch, n, mb, a.seed + rank, dev)
+    off = torch.arange(n + 1, dtype=torch.int64, device=dev) * mb
+    codec = TdtCodec(TDTConfig(sample_fraction=1.0), device=local)
+    codec.set_metrics(10.0, 1.0, 0.5)  # slow network → compression on (tdt_compression.hpp:200)
+    codec.set_size_hint(mb)
+    cap = n * codec.encode_bound(mb)
+    enc = torch.empty(cap, dtype=torch.uint8, device=dev)
+    eoff = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    est = torch.empty(n, dtype=torch.int32, device=dev)
+    dec = torch.empty(n * mb, dtype=torch.uint8, device=dev)
+    doff = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    dst = torch.empty(n, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def step(ev=None):
+        if ev:
+            ev[0].record(stream)
+        codec.encode_batch(data, off, out=enc, out_offsets=eoff, status=est)
+        if ev:
+            ev[1].record(stream)
+        codec.decode_batch(enc, eoff, out=dec, out_offsets=doff, status=dst)
+        if ev:
+            ev[2].record(stream)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    # correctness of the measured configuration (size-independent property): round trip
+    ok = bool(torch.equal(dec, data)) and int(est.abs().sum()) == 0 and int(dst.abs().sum()) == 0
+    enc_bytes = int(eoff[-1].item())
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(a.steps)]
+    t0 = time.perf_counter()
+    for k in range(a.steps):
+        step(evs[k])
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    t_enc = sum(e[0].elapsed_time(e[1]) for e in evs) / a.steps  # ms, encode launch incl. memset
+    t_dec = sum(e[1].elapsed_time(e[2]) for e in evs) / a.steps
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        okt = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+        ok = bool(okt.item())
+
+    payload = n * mb
+    ms_per_step = elapsed / a.steps * 1e3
+    value = world * payload * a.steps / elapsed / 2**30
+
+    host = None
+    if a.host_inclusive and rank == 0:
+        host = host_inclusive(torch, codec, data, off, n, mb, enc_bytes)
+
+    if rank == 0:
+        alg = payload + enc_bytes  # algorithmic bytes per launch (read input once, write output once)
+        dom, t_dom = ("tdt_encode_kernel", t_enc) if t_enc >= t_dec else ("tdt_decode_kernel", t_dec)
+        achieved = alg / (t_dom * 1e-3) / 1e9
+        key = "c3_%dx%d" % (n, mb)
+        tr = load_traffic(key)
+        traffic = None
+        if tr and dom in tr.get("kernels", {}):
+            traffic = tr["kernels"][dom].get("hbm_bytes_per_launch")
+        cpu = None
+        if a.cpu_seconds > 0:
+            thr = a.cpu_threads or min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "1024")))
+            cpu = cpu_baseline(data, mb, a.cpu_seconds, thr)
+        line = {
+            "metric": "TDT encode+decode GiB/s (device-resident), 64 KiB msgs, 1/2/4/8 MI355X",
+            "value": round(value, 3),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (device-generated gradient-like float32: 70% zeros, N(0,0.01); seed 0x5EED0002+rank)",
+            "config": {"workload": "C3: %d x %d B float32 gradient-like messages per GPU, encode+decode" % (n, mb),
+                       "msgs_per_gpu": n, "msg_bytes": mb, "word_size": 4, "sample_fraction": 1.0,
+                       "bandwidth_mbps": 10.0, "parallelism": "independent message shards (dp%d)" % world},
+            "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": traffic,
+                         "algorithmic_bytes_per_launch": alg},
+            "kernels_ms": {"encode": round(t_enc, 4), "decode": round(t_dec, 4)},
+            "compression_ratio": round(payload / enc_bytes, 4),
+            "roundtrip_ok": ok,
+            "cpu_baseline": cpu,
+        }
+        if host:
+            line["host_inclusive"] = host
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def host_inclusive(torch, codec, data, off, n, mb, enc_bytes, reps=3):
+    """Pinned host → device → encode → host, and back through decode (the TCP socket-buffer
+    path); returns GiB/s of payload for each direction over a sub-batch."""
+    m = min(n, 32768)
+    src = torch.empty(m * mb, dtype=torch.uint8, pin_memory=True)
+    src.copy_(data[: m * mb])
+    moff = off[: m + 1].clone()
+    dv = torch.empty_like(data[: m * mb])
+    cap = m * codec.encode_bound(mb)
+    enc = torch.empty(cap, dtype=torch.uint8, device=data.device)
+    eoff = torch.empty(m + 1, dtype=torch.int64, device=data.device)
+    est = torch.empty(m, dtype=torch.int32, device=data.device)
+    henc = torch.empty(cap, dtype=torch.uint8, pin_memory=True)
+    dec = torch.empty(m * mb, dtype=torch.uint8, device=data.device)
+    doff = torch.empty(m + 1, dtype=torch.int64, device=data.device)
+    dst = torch.empty(m, dtype=torch.int32, device=data.device)
+    hdec = torch.empty(m * mb, dtype=torch.uint8, pin_memory=True)
+    torch.cuda.synchronize()
+    te, td = [], []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        dv.copy_(src, non_blocking=True)
+        codec.encode_batch(dv, moff, out=enc, out_offsets=eoff, status=est)
+        nb = int(eoff[-1].item())
+        henc[:nb].copy_(enc[:nb], non_blocking=True)
+        torch.cuda.synchronize()
+        te.append(time.perf_counter() - t0)
+        t0 = time.perf_counter()
+        enc[:nb].copy_(henc[:nb], non_blocking=True)
+        codec.decode_batch(enc, eoff, out=dec, out_offsets=doff, status=dst)
+        hdec.copy_(dec, non_blocking=True)
+        torch.cuda.synchronize()
+        td.append(time.perf_counter() - t0)
+    ok = bool(torch.equal(hdec, src))
+    b = m * mb
+    return {"msgs": m, "encode_GiBps": round(b / min(te) / 2**30, 3), "decode_GiBps": round(b / min(td) / 2**30, 3),
+            "roundtrip_GiBps": round(b / (min(te) + min(td)) / 2**30, 3), "ok": ok,
+            "note": "pinned H2D + kernel + D2H, payload bytes / wall"}
+
+
+if __name__ == "__main__":
+    main()

@@ -134,6 +134,11 @@ int tdt_encode_host(tdt_ctx *ctx, const uint8_t *h_in, const uint64_t *h_in_off,
 int tdt_decode_host(tdt_ctx *ctx, const uint8_t *h_in, const uint64_t *h_in_off, uint32_t n_msgs,
                     uint8_t *h_out, uint64_t out_cap, uint64_t *h_out_off, int32_t *h_status);
 
+/* Device-side invariant flags of the most recent batch on this context (synchronises the
+ * device): bit0 look-back timeout, bit1 staging-index guard, bit2 flush-bound guard.  Always
+ * 0 for a correct build; the guards turn a logic error into a flag instead of a wild write. */
+int tdt_ctx_error_flags(tdt_ctx *ctx, uint32_t *flags);
+
 /* Text of the last error on this thread ("" if none). */
 const char *tdt_last_error(void);
 /* Human-readable status name; for TDT_E_SHORT / TDT_E_MAGIC the reference's exception text. */

@@ -114,7 +114,7 @@ int encode_common(tdt_ctx *c, int mode, const uint8_t *d_in, const uint64_t *d_i
                   int32_t *d_status, uint32_t *d_hist, double *d_ent, int32_t *d_map, void *stream) {
     if (!c) return set_err(TDT_E_ARG, "null context");
     if (n_msgs == 0) return TDT_OK;
-    if (!d_in || !d_in_off) return set_err(TDT_E_ARG, "null input");
+    if (!d_in_off) return set_err(TDT_E_ARG, "null input offsets");  // d_in may be null: all-empty batch
     if (mode != psy::MODE_ANALYZE && (!d_out || !d_out_off)) return set_err(TDT_E_ARG, "null output");
     if (mode == psy::MODE_MAPPED && !d_mapping) return set_err(TDT_E_ARG, "null mapping");
     hipStream_t s = (hipStream_t)stream;
@@ -134,7 +134,7 @@ int encode_common(tdt_ctx *c, int mode, const uint8_t *d_in, const uint64_t *d_i
     a.ent_out = d_ent;
     a.map_out = d_map;
     a.ticket = reinterpret_cast<uint32_t *>(c->ws);
-    a.timeout = reinterpret_cast<uint32_t *>(c->ws) + 1;
+    a.errflags = reinterpret_cast<uint32_t *>(c->ws) + 1;
     a.lookback = reinterpret_cast<uint64_t *>(c->ws + kCounterBytes);
     a.min_tensor = c->cfg.min_tensor_size;
     a.policy_on = policy_on(c) ? 1 : 0;
@@ -151,7 +151,7 @@ int decode_common(tdt_ctx *c, bool sizes_only, const uint8_t *d_in, const uint64
                   void *stream) {
     if (!c) return set_err(TDT_E_ARG, "null context");
     if (n_msgs == 0) return TDT_OK;
-    if (!d_in || !d_in_off) return set_err(TDT_E_ARG, "null input");
+    if (!d_in_off) return set_err(TDT_E_ARG, "null input offsets");
     if (!sizes_only && (!d_out_off)) return set_err(TDT_E_ARG, "null output offsets");
     if (sizes_only && !d_sizes) return set_err(TDT_E_ARG, "null sizes");
     hipStream_t s = (hipStream_t)stream;
@@ -168,7 +168,7 @@ int decode_common(tdt_ctx *c, bool sizes_only, const uint8_t *d_in, const uint64
     a.status = d_status;
     a.sizes_out = d_sizes;
     a.ticket = reinterpret_cast<uint32_t *>(c->ws);
-    a.timeout = reinterpret_cast<uint32_t *>(c->ws) + 1;
+    a.errflags = reinterpret_cast<uint32_t *>(c->ws) + 1;
     a.lookback = reinterpret_cast<uint64_t *>(c->ws + kCounterBytes);
     const bool small = c->size_hint.load() <= 4096;
     if (sizes_only) {
@@ -237,10 +237,10 @@ int host_path(tdt_ctx *c, bool encode, const uint8_t *h_in, const uint64_t *h_in
     if (st) return st;
     HIPCHK(hipMemcpyAsync(h_out_off, d + o_ooff, 8ull * (n_msgs + 1), hipMemcpyDeviceToHost, s));
     if (h_status) HIPCHK(hipMemcpyAsync(h_status, d + o_st, 4ull * n_msgs, hipMemcpyDeviceToHost, s));
-    uint32_t timeout = 0;
-    HIPCHK(hipMemcpyAsync(&timeout, c->ws + 4, 4, hipMemcpyDeviceToHost, s));
+    uint32_t flags = 0;
+    HIPCHK(hipMemcpyAsync(&flags, c->ws + 4, 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
-    if (timeout) return set_err(TDT_E_HIP, "look-back timeout");
+    if (flags) return set_err(TDT_E_HIP, "device error flags " + std::to_string(flags));
     const uint64_t produced = std::min<uint64_t>(h_out_off[n_msgs], out_cap);
     if (produced) HIPCHK(hipMemcpy(h_out, d + o_out, produced, hipMemcpyDeviceToHost));
     return TDT_OK;
@@ -348,6 +348,16 @@ int tdt_encode_host(tdt_ctx *ctx, const uint8_t *h_in, const uint64_t *h_in_off,
 int tdt_decode_host(tdt_ctx *ctx, const uint8_t *h_in, const uint64_t *h_in_off, uint32_t n_msgs, uint8_t *h_out,
                     uint64_t out_cap, uint64_t *h_out_off, int32_t *h_status) {
     return host_path(ctx, false, h_in, h_in_off, n_msgs, h_out, out_cap, h_out_off, h_status);
+}
+
+int tdt_ctx_error_flags(tdt_ctx *ctx, uint32_t *flags) {
+    if (!ctx || !flags) return set_err(TDT_E_ARG, "null argument");
+    *flags = 0;
+    if (!ctx->ws) return TDT_OK;
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpy(flags, ctx->ws + 4, 4, hipMemcpyDeviceToHost));
+    return TDT_OK;
 }
 
 const char *tdt_last_error(void) { return g_err.c_str(); }

@@ -31,7 +31,7 @@ struct DecodeArgs {
     uint64_t *sizes_out;  // sizes-only mode
     uint64_t *lookback;
     uint32_t *ticket;
-    uint32_t *timeout;
+    uint32_t *errflags;
 };
 
 constexpr int kMaxRef = 16;  // referenced streams <= word_size <= 16
@@ -181,7 +181,7 @@ __global__ __launch_bounds__(TEAM) void tdt_decode_kernel(DecodeArgs a) {
             a.sizes_out[msg] = osize;
             if (a.status) a.status[msg] = (int32_t)st;
         } else {
-            const uint64_t b = lookback_excl(a.lookback, msg, osize, a.timeout);
+            const uint64_t b = lookback_excl(a.lookback, msg, osize, a.errflags);
             *reinterpret_cast<uint64_t *>(misc + D_BASE) = b;
             const bool fits = b + osize <= a.out_cap;
             a.out_off[msg] = b;

@@ -61,7 +61,7 @@ struct EncodeArgs {
     int32_t *map_out;
     uint64_t *lookback;
     uint32_t *ticket;
-    uint32_t *timeout;
+    uint32_t *errflags;  // bit0 look-back timeout, bit1 staging index, bit2 flush bound
     uint64_t min_tensor;
     int32_t policy_on;  // bandwidth < threshold && cpu <= threshold (host-evaluated atomics)
 };
@@ -153,7 +153,7 @@ __global__ __launch_bounds__(TEAM) void tdt_encode_kernel(EncodeArgs a) {
         if constexpr (MODE != MODE_ANALYZE) {
             const uint64_t E = n + 4;
             if (tid == 0) {
-                uint64_t b = lookback_excl(a.lookback, msg, E, a.timeout);
+                uint64_t b = lookback_excl(a.lookback, msg, E, a.errflags);
                 *reinterpret_cast<uint64_t *>(misc + M_BASE) = b;
             }
             team_sync<W>();
@@ -226,7 +226,7 @@ __global__ __launch_bounds__(TEAM) void tdt_encode_kernel(EncodeArgs a) {
         if (misc[M_STATUS]) {
             // invalid caller mapping: publish an empty output for this message
             if (tid == 0) {
-                uint64_t b = lookback_excl(a.lookback, msg, 0, a.timeout);
+                uint64_t b = lookback_excl(a.lookback, msg, 0, a.errflags);
                 a.out_off[msg] = b;
                 if (msg == a.n_msgs - 1) a.out_off[a.n_msgs] = b;
                 if (a.status) a.status[msg] = ST_BAD_MAPPING;
@@ -400,8 +400,8 @@ __global__ __launch_bounds__(TEAM) void tdt_encode_kernel(EncodeArgs a) {
         uint32_t scan_par = 0;
 
         // one round of the count pass (EMIT=false) or the emit pass (EMIT=true)
-        auto round = [&](uint32_t r, const uint4 d, auto emit_tag, uint64_t out_base, const uint32_t *sdata)
-                         __attribute__((always_inline)) {
+        auto round = [&](uint32_t r, const uint4 d, auto emit_tag, uint64_t out_base, const uint32_t *sdata,
+                         uint64_t E) __attribute__((always_inline)) {
             constexpr bool EMIT = decltype(emit_tag)::value;
             const uint32_t g = r * TEAM + tid;
             const bool last_group = 16ull * (g + 1) >= n;
@@ -459,18 +459,17 @@ __global__ __launch_bounds__(TEAM) void tdt_encode_kernel(EncodeArgs a) {
             ++scan_par;
             if (EMIT) {
                 uint32_t k0[2], ra[2];
-                uint8_t *reg[2];
 #pragma unroll
                 for (int c = 0; c < 2; ++c) {
                     k0[c] = carry_P[c] - misc[M_DANG + c];
                     const uintptr_t dst = (uintptr_t)a.out + out_base + sdata[c] + 2ull * k0[c];
                     ra[c] = (uint32_t)(dst & 15);
-                    reg[c] = uni + c * Lay::REGION + ra[c];
                 }
 #pragma unroll
                 for (int c = 0; c < 2; ++c) {
                     uint32_t em = endm[c];
                     const uint32_t pb = carry_P[c] + sv[c];
+                    const uint32_t rbase = Lay::OFF_UNION + c * Lay::REGION + ra[c];
                     while (em) {
                         const uint32_t j = lobit(em);
                         em &= em - 1u;
@@ -486,28 +485,36 @@ __global__ __launch_bounds__(TEAM) void tdt_encode_kernel(EncodeArgs a) {
                             idx = pb - 1u;
                         }
                         const uint32_t val = byte_of(x[c].s[0], x[c].s[1], x[c].s[2], x[c].s[3], j);
-                        uint8_t *p = reg[c] + 2u * (idx - k0[c]);
-                        p[0] = (uint8_t)cnt;
-                        p[1] = (uint8_t)val;
+                        const uint32_t rel = idx - k0[c];
+                        if (rel < st[2 + c]) {  // always true for a consistent round
+                            smem[rbase + 2u * rel] = (uint8_t)cnt;
+                            smem[rbase + 2u * rel + 1u] = (uint8_t)val;
+                        } else {
+                            atomicOr(a.errflags, 2u);
+                        }
                     }
                 }
                 team_sync<W>();
                 // flush both regions: LDS (congruent mod 16 with the destination) → global
 #pragma unroll
                 for (int c = 0; c < 2; ++c) {
-                    const uint32_t len = 2u * st[2 + c];
+                    uint32_t len = 2u * st[2 + c];
+                    if (len && sdata[c] + 2ull * k0[c] + len > E) {  // never for a consistent round
+                        if (tid == 0) atomicOr(a.errflags, 4u);
+                        len = 0;
+                    }
                     if (len) {
                         uint8_t *dst = a.out + out_base + sdata[c] + 2ull * k0[c];
-                        const uint8_t *src = reg[c];
+                        const uint32_t sb = Lay::OFF_UNION + c * Lay::REGION + ra[c];
                         const uint32_t head0 = (16u - ra[c]) & 15u;
                         const uint32_t head = head0 < len ? head0 : len;
                         const uint32_t body = (len - head) & ~15u;
-                        if ((uint32_t)tid < head) dst[tid] = src[tid];
+                        if ((uint32_t)tid < head) dst[tid] = smem[sb + tid];
                         for (uint32_t k = tid; k < body / 16; k += TEAM)
                             *reinterpret_cast<uint4 *>(dst + head + 16 * k) =
-                                *reinterpret_cast<const uint4 *>(src + head + 16 * k);
+                                *reinterpret_cast<const uint4 *>(smem + sb + head + 16 * k);
                         const uint32_t tail = len - head - body;
-                        if ((uint32_t)tid < tail) dst[head + body + tid] = src[head + body + tid];
+                        if ((uint32_t)tid < tail) dst[head + body + tid] = smem[sb + head + body + tid];
                     }
                 }
             }
@@ -517,12 +524,12 @@ __global__ __launch_bounds__(TEAM) void tdt_encode_kernel(EncodeArgs a) {
 
         // ---------------------------------------------------------- pass A: count pairs
         const uint32_t nosd[2] = {0, 0};
-        for_rounds([&](uint32_t r, const uint4 d) __attribute__((always_inline)) { round(r, d, std::false_type{}, 0, nosd); });
+        for_rounds([&](uint32_t r, const uint4 d) __attribute__((always_inline)) { round(r, d, std::false_type{}, 0, nosd, 0); });
         const uint32_t P0 = carry_P[0], P1 = sd.ns > 1 ? carry_P[1] : 0;
         const uint32_t hdr = 20 + 4 * WS;
         const uint64_t E = hdr + (4 + 2ull * P0) + (sd.ns > 1 ? 4 + 2ull * P1 : 0);
         if (tid == 0) {
-            uint64_t b = lookback_excl(a.lookback, msg, E, a.timeout);
+            uint64_t b = lookback_excl(a.lookback, msg, E, a.errflags);
             *reinterpret_cast<uint64_t *>(misc + M_BASE) = b;
         }
         team_sync<W>();
@@ -537,15 +544,15 @@ __global__ __launch_bounds__(TEAM) void tdt_encode_kernel(EncodeArgs a) {
         // header :84-106 and stream length words :110-112
         uint8_t *dst = a.out + ob;
         const uint32_t sdata[2] = {hdr + 4, hdr + 4 + 2 * P0 + 4};
-        if ((uint32_t)tid < hdr) {
-            const int f = tid >> 2, sh = 8 * (tid & 3);
+        for (uint32_t t = tid; t < hdr; t += TEAM) {
+            const int f = t >> 2, sh = 8 * (t & 3);
             uint32_t v;
             if (f == 0) v = kMagicTDT;
             else if (f == 1) v = n32;
             else if (f == 2) v = sd.ns;
             else if (f == 3 || f == 4) v = WS;
             else v = misc[M_MAP + (f - 5)];
-            dst[tid] = (uint8_t)(v >> sh);
+            dst[t] = (uint8_t)(v >> sh);
         }
         if (tid < 8) {
             const int c = tid >> 2, sh = 8 * (tid & 3);
@@ -557,7 +564,7 @@ __global__ __launch_bounds__(TEAM) void tdt_encode_kernel(EncodeArgs a) {
         // ---------------------------------------------------------- pass B: emit pairs
         carry_max[0] = carry_max[1] = 0;
         carry_P[0] = carry_P[1] = 0;
-        for_rounds([&](uint32_t r, const uint4 d) __attribute__((always_inline)) { round(r, d, std::true_type{}, ob, sdata); });
+        for_rounds([&](uint32_t r, const uint4 d) __attribute__((always_inline)) { round(r, d, std::true_type{}, ob, sdata, E); });
     }
 }
 

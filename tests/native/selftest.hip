@@ -1,0 +1,51 @@
+// tests/native/selftest.hip — hardware-semantics self-test of the device primitives in
+// psyne_amd/csrc/tdt_device.h (DPP wave scans, team scans, SWAR run-start masks, v_perm /
+// v_alignbyte operand order).  Test infrastructure: every access is within fixed-size
+// buffers sized by the caller, so a wrong primitive shows up as a wrong value, never a fault.
+#include "../../psyne_amd/csrc/tdt_device.h"
+
+using namespace psy;
+
+// in: 256 uint32; out layout (uint32):
+//   [0,256)    wave inclusive add-scan (4 waves independently)
+//   [256,512)  wave inclusive max-scan
+//   [512,768)  team exclusive add-scan (W=4), [768] team total
+//   [769,1025) team exclusive max-scan (W=4), [1025] total
+//   [1026,1090) W=1 exclusive add-scan of the first 64 inputs, [1090] total
+//   [1091,1155) neq_prev_mask4(in[l], in[l+64]) for lanes 0..63
+//   [1155,1219) perm(in[l], in[l+64], sel[l%8])
+//   [1219,1283) alignbyte(in[l], in[l+64], 3)
+//   [1283,1347) wave_shift_up1(in[l])
+__global__ __launch_bounds__(256) void selftest_kernel(const uint32_t *in, uint32_t *out) {
+    __shared__ uint32_t slots[2 * 4 * 4];
+    const int t = threadIdx.x, lane = t & 63;
+    const uint32_t x = in[t];
+    out[t] = wave_incl_scan<OpAdd>(x);
+    out[256 + t] = wave_incl_scan<OpMax>(x);
+    uint32_t v[1] = {x}, tot[1];
+    team_excl_scan<4, 1, OpAdd>(v, tot, slots);
+    out[512 + t] = v[0];
+    if (t == 0) out[768] = tot[0];
+    uint32_t m[1] = {x}, mt[1];
+    team_excl_scan<4, 1, OpMax>(m, mt, slots + 16);
+    out[769 + t] = m[0];
+    if (t == 0) out[1025] = mt[0];
+    if (t < 64) {
+        uint32_t w[1] = {x}, wt[1];
+        team_excl_scan<1, 1, OpAdd>(w, wt, nullptr);
+        out[1026 + t] = w[0];
+        if (t == 0) out[1090] = wt[0];
+        const uint32_t y = in[t + 64];
+        out[1091 + t] = neq_prev_mask4(x, y);
+        const uint32_t sels[8] = {0x03020100u, 0x07060504u, 0x0c0c0c0cu, 0x0400070cu,
+                                  0x01050c02u, 0x0c0c0706u, 0x00000000u, 0x07070707u};
+        out[1155 + t] = __builtin_amdgcn_perm(x, y, sels[lane & 7]);
+        out[1219 + t] = __builtin_amdgcn_alignbyte(x, y, 3);
+        out[1283 + t] = wave_shift_up1(x);
+    }
+}
+
+extern "C" int selftest_run(const uint32_t *d_in, uint32_t *d_out) {
+    hipLaunchKernelGGL(selftest_kernel, dim3(1), dim3(256), 0, 0, d_in, d_out);
+    return hipDeviceSynchronize() == hipSuccess ? 0 : 1;
+}

@@ -1,0 +1,60 @@
+"""Runs FIRST among the GPU tests: checks the hardware semantics of the device primitives
+the codec kernels are built from (tests/native/selftest.hip) against host expectations."""
+import ctypes as C
+import pathlib
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+LIB = pathlib.Path(__file__).resolve().parent / "native" / "libtdt_selftest.so"
+
+
+def host_perm(hi, lo, sel):
+    src = int(lo) | (int(hi) << 32)
+    out = 0
+    for t in range(4):
+        s = (sel >> (8 * t)) & 0xFF
+        b = (src >> (8 * s)) & 0xFF if s < 8 else 0
+        out |= b << (8 * t)
+    return out
+
+
+def host_mask4(x, below):
+    prev = [(below >> 24) & 0xFF] + [(x >> (8 * i)) & 0xFF for i in range(3)]
+    cur = [(x >> (8 * i)) & 0xFF for i in range(4)]
+    return sum((1 << i) for i in range(4) if cur[i] != prev[i])
+
+
+def test_primitives():
+    assert torch.cuda.is_available()
+    lib = C.CDLL(str(LIB))
+    rng = np.random.default_rng(5)
+    x = rng.integers(0, 1000, 256).astype(np.uint32)
+    x[64:128] = rng.integers(0, 4, 64) * 0x01010101  # byte-equal patterns for the mask test
+    x[5] = x[69] = 0x11223344
+    d_in = torch.from_numpy(x.view(np.int32).copy()).cuda()
+    d_out = torch.zeros(1400, dtype=torch.int32, device="cuda")
+    assert lib.selftest_run(C.c_void_p(d_in.data_ptr()), C.c_void_p(d_out.data_ptr())) == 0
+    o = d_out.cpu().numpy().view(np.uint32)
+    xs = x.astype(np.uint64)
+    for w in range(4):
+        seg = xs[64 * w:64 * w + 64]
+        assert np.array_equal(o[64 * w:64 * w + 64], np.cumsum(seg).astype(np.uint32)), "wave add-scan"
+        assert np.array_equal(o[256 + 64 * w:256 + 64 * w + 64], np.maximum.accumulate(seg).astype(np.uint32)), "wave max-scan"
+    ex = np.concatenate([[0], np.cumsum(xs)[:-1]]).astype(np.uint32)
+    assert np.array_equal(o[512:768], ex), "team add-scan"
+    assert o[768] == np.uint32(xs.sum())
+    exm = np.concatenate([[0], np.maximum.accumulate(xs)[:-1]]).astype(np.uint32)
+    assert np.array_equal(o[769:1025], exm), "team max-scan"
+    assert o[1025] == x.max()
+    assert np.array_equal(o[1026:1090], np.concatenate([[0], np.cumsum(xs[:64])[:-1]]).astype(np.uint32)), "W=1 scan"
+    assert o[1090] == np.uint32(xs[:64].sum())
+    sels = [0x03020100, 0x07060504, 0x0C0C0C0C, 0x0400070C, 0x01050C02, 0x0C0C0706, 0, 0x07070707]
+    for l in range(64):
+        assert o[1091 + l] == host_mask4(int(x[l]), int(x[l + 64])), ("mask", l)
+        assert o[1155 + l] == host_perm(int(x[l]), int(x[l + 64]), sels[l & 7]), ("perm", l)
+        assert o[1219 + l] == (((int(x[l]) << 32 | int(x[l + 64])) >> 24) & 0xFFFFFFFF), ("alignbyte", l)
+        assert o[1283 + l] == (x[l - 1] if l else 0), ("shift_up", l)
