@@ -139,6 +139,11 @@ int tdt_decode_host(tdt_ctx *ctx, const uint8_t *h_in, const uint64_t *h_in_off,
  * 0 for a correct build; the guards turn a logic error into a flag instead of a wild write. */
 int tdt_ctx_error_flags(tdt_ctx *ctx, uint32_t *flags);
 
+/* Host-memory analyze (analyze_data :206-222): h_entropy n*ws doubles, h_mapping n*ws int32
+ * (either may be NULL).  Blocks the calling thread. */
+int tdt_analyze_host(tdt_ctx *ctx, const uint8_t *h_in, const uint64_t *h_in_off, uint32_t n_msgs,
+                     double *h_entropy, int32_t *h_mapping, int32_t *h_status);
+
 /* Text of the last error on this thread ("" if none). */
 const char *tdt_last_error(void);
 /* Human-readable status name; for TDT_E_SHORT / TDT_E_MAGIC the reference's exception text. */

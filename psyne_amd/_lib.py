@@ -43,6 +43,7 @@ SIGNATURES = {
     "tdt_analyze_batch": (C.c_int, [_vp, _vp, _vp, C.c_uint32, _vp, _vp, _vp, _vp, _vp]),
     "tdt_encode_host": (C.c_int, [_vp, _vp, _vp, C.c_uint32, _vp, C.c_uint64, _vp, _vp]),
     "tdt_decode_host": (C.c_int, [_vp, _vp, _vp, C.c_uint32, _vp, C.c_uint64, _vp, _vp]),
+    "tdt_analyze_host": (C.c_int, [_vp, _vp, _vp, C.c_uint32, _vp, _vp, _vp]),
     "tdt_ctx_error_flags": (C.c_int, [_vp, C.POINTER(C.c_uint32)]),
     "tdt_last_error": (C.c_char_p, []),
     "tdt_status_string": (C.c_char_p, [C.c_int]),

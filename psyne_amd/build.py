@@ -39,6 +39,31 @@ def build(force: bool = False, verbose: bool = False) -> pathlib.Path:
     return LIB
 
 
+CPP_TEST_SRC = ROOT / "tests" / "cpp" / "test_protocol.cpp"
+CPP_TEST_BIN = ROOT / "tests" / "cpp" / "test_protocol"
+SELFTEST_SRC = ROOT / "tests" / "native" / "selftest.hip"
+SELFTEST_LIB = ROOT / "tests" / "native" / "libtdt_selftest.so"
+
+
+def build_tests(verbose: bool = False):
+    """Test-only native artefacts: the C++ Protocol drop-in test and the primitives self-test."""
+    if not CPP_TEST_BIN.exists() or CPP_TEST_BIN.stat().st_mtime < max(
+            CPP_TEST_SRC.stat().st_mtime, (ROOT / "include/psyne_amd/hip_tdt_protocol.hpp").stat().st_mtime,
+            LIB.stat().st_mtime):
+        cmd = ["g++", "-std=c++20", "-O2", "-I", str(ROOT / "include"), str(CPP_TEST_SRC), "-o", str(CPP_TEST_BIN),
+               "-L", str(PKG), "-lpsyne_tdt", "-Wl,-rpath," + str(PKG), "-Wl,-rpath,$ORIGIN/../../psyne_amd"]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.check_call(cmd)
+    if not SELFTEST_LIB.exists() or SELFTEST_LIB.stat().st_mtime < max(
+            SELFTEST_SRC.stat().st_mtime, (CSRC / "tdt_device.h").stat().st_mtime):
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-shared", str(SELFTEST_SRC), "-o", str(SELFTEST_LIB)]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.check_call(cmd)
+
+
 if __name__ == "__main__":
     build(force="--force" in sys.argv, verbose=True)
+    build_tests(verbose=True)
     print(LIB)

@@ -13,6 +13,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <vector>
 
 #include "tdt_decode.h"
 #include "tdt_encode.h"
@@ -357,6 +358,40 @@ int tdt_ctx_error_flags(tdt_ctx *ctx, uint32_t *flags) {
     HIPCHK(hipSetDevice(ctx->device));
     HIPCHK(hipDeviceSynchronize());
     HIPCHK(hipMemcpy(flags, ctx->ws + 4, 4, hipMemcpyDeviceToHost));
+    return TDT_OK;
+}
+
+int tdt_analyze_host(tdt_ctx *ctx, const uint8_t *h_in, const uint64_t *h_in_off, uint32_t n_msgs, double *h_entropy,
+                     int32_t *h_mapping, int32_t *h_status) {
+    if (!ctx) return set_err(TDT_E_ARG, "null context");
+    if (n_msgs == 0) return TDT_OK;
+    HIPCHK(hipSetDevice(ctx->device));
+    const uint64_t in_bytes = h_in_off[n_msgs] - h_in_off[0];
+    const size_t ws = (size_t)ctx->cfg.word_size;
+    const size_t o_off = align_up(in_bytes, 256);
+    const size_t o_ent = align_up(o_off + 8ull * (n_msgs + 1), 256);
+    const size_t o_map = align_up(o_ent + 8ull * n_msgs * ws, 256);
+    const size_t o_st = align_up(o_map + 4ull * n_msgs * ws, 256);
+    const size_t total = align_up(o_st + 4ull * n_msgs, 256);
+    int st;
+    {
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        st = ensure_host_dev(ctx, total);
+    }
+    if (st) return st;
+    uint8_t *d = ctx->h_dev;
+    std::vector<uint64_t> tmp(n_msgs + 1);
+    for (uint32_t i = 0; i <= n_msgs; ++i) tmp[i] = h_in_off[i] - h_in_off[0];
+    HIPCHK(hipMemcpy(d, h_in + h_in_off[0], in_bytes, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(d + o_off, tmp.data(), 8ull * (n_msgs + 1), hipMemcpyHostToDevice));
+    st = encode_common(ctx, psy::MODE_ANALYZE, d, reinterpret_cast<uint64_t *>(d + o_off), n_msgs, nullptr, nullptr,
+                       0, nullptr, reinterpret_cast<int32_t *>(d + o_st), nullptr,
+                       reinterpret_cast<double *>(d + o_ent), reinterpret_cast<int32_t *>(d + o_map), nullptr);
+    if (st) return st;
+    HIPCHK(hipDeviceSynchronize());
+    if (h_entropy) HIPCHK(hipMemcpy(h_entropy, d + o_ent, 8ull * n_msgs * ws, hipMemcpyDeviceToHost));
+    if (h_mapping) HIPCHK(hipMemcpy(h_mapping, d + o_map, 4ull * n_msgs * ws, hipMemcpyDeviceToHost));
+    if (h_status) HIPCHK(hipMemcpy(h_status, d + o_st, 4ull * n_msgs, hipMemcpyDeviceToHost));
     return TDT_OK;
 }
 

@@ -341,3 +341,13 @@ def test_protocol_mirror():
     p.analyze_data(m, len(m))
     _, e, _ = orc.analyze(np.frombuffer(m, np.uint8))
     assert p.get_average_entropy() == sum(float(v) for v in e) / 4
+
+
+def test_cpp_protocol_dropin():
+    """The header-only C++ HipTDTCompressionProtocol, used through psyne's Protocol concept."""
+    import pathlib
+    import subprocess
+    exe = pathlib.Path(__file__).resolve().parent / "cpp" / "test_protocol"
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "cpp protocol OK" in r.stdout

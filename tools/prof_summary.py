@@ -12,7 +12,8 @@ import sys
 
 def rows_from_db(db):
     c = sqlite3.connect(db)
-    return [(r[0], int(r[1]), float(r[2]), float(r[3]), float(r[4]))
+    # the rocpd top_kernels view reports durations in microseconds; normalise to ns
+    return [(r[0], int(r[1]), float(r[2]) * 1e3, float(r[3]) * 1e3, float(r[4]))
             for r in c.execute("select name,total_calls,total_duration,average,percentage from top_kernels")]
 
 
