@@ -11,22 +11,25 @@
 //   simple_rle_compress    :557-582  (count <= 255, value) pairs
 //   TDTEncodedData::serialize :81-117
 //
-// Work decomposition (DESIGN.md §Encode): one TEAM-thread workgroup per message, message ids
-// claimed through an atomic ticket.  A message is a sequence of 16-byte GROUPS; group g
-// lives in thread (g mod TEAM) of round (g / TEAM) — every round is one fully coalesced
-// 16 B/lane sweep.  Messages of up to G rounds stay in VGPRs across all three passes
-// (histogram, count, emit), so HBM sees each payload byte once.
+// Work decomposition (DESIGN.md §4): one TEAM-thread workgroup per message, message ids
+// claimed through an atomic ticket.  A message is a sequence of 16-byte GROUPS.  Wave w of
+// the team owns the contiguous group range [w·RW·64, (w+1)·RW·64): round r of the wave is
+// one coalesced 1 KiB sweep (lane l ↔ group (w·RW + r)·64 + l).  Because every wave owns a
+// contiguous stretch of the byte streams, all per-round scans are wave-level DPP scans with
+// a uniform running carry; the team synchronises only to exchange wave carries (twice).
+// Messages of up to G rounds per wave stay in VGPRs across all passes (the round arrays are
+// rotated, never dynamically indexed), so HBM sees each payload byte once.
 //
-// RLE in parallel: for stream c a group holds L = words*k_c consecutive stream bytes,
-// packed into 4 dwords.  Run starts come from a SWAR byte compare against the byte before
-// (neq_prev_mask4).  The 255-count cap only splits the run that is carried INTO a group
-// (runs starting inside a 16-byte group cannot reach 255 there), so one max-scan of "last
-// run start" gives every group its carried run start and at most one cap boundary.  A
-// sum-scan of chunk starts gives every pair its index; pairs are emitted at chunk ENDS
-// (count known locally) into an LDS staging window whose start is congruent to its
-// destination mod 16, then flushed with 16-byte stores.  Output offsets across messages
-// come from a single-pass decoupled look-back (tdt_device.h), so the batch output is
-// compacted with no extra pass.
+// RLE in parallel, per group and stream c (L = words·k_c consecutive stream bytes):
+//   * run starts: SWAR byte compare against the byte before (neq_prev_mask4);
+//   * the 255 cap only splits the run carried INTO a group (a run starting inside a 16-byte
+//     group cannot reach 255 there), so a max-scan of the last run start gives every group
+//     its carried run start and at most one cap boundary → chunk-start mask (kept in VGPRs);
+//   * pairs are indexed by a sum-scan of chunk starts and emitted at chunk ENDS (the count
+//     is known locally), slot by slot with predicated LDS stores into a per-wave window that
+//     is congruent mod 16 with its destination, then flushed with 16-byte stores — the emit
+//     pass has no workgroup barrier at all.
+// Output offsets across messages come from a single-pass decoupled look-back.
 #pragma once
 #include "tdt_device.h"
 #include "tdt_log2.h"
@@ -72,11 +75,12 @@ struct EncLayout {
     static constexpr int WPG = 16 / WS;  // words per 16-byte group
     static constexpr int TB = (TEAM >= 256) ? (WS < 4 ? WS : 4) : (WS < 2 ? WS : 2);
     static constexpr int HIST = WS * 256 * 4;
-    static constexpr int REGION = 2 * TEAM * 16 + 16;
-    static constexpr int STAGE = 2 * REGION;
+    static constexpr int WREGION = 2 * 64 * 16 + 16;  // one stream's pairs of one wave-round
+    static constexpr int WSTAGE = 2 * WREGION;        // both streams, per wave
+    static constexpr int STAGE = W * WSTAGE;
     static constexpr int TERMS = TB * 256 * 16;
     static constexpr int UNION = STAGE > TERMS ? STAGE : TERMS;
-    static constexpr int SLOTS = 2 * W * 4 * 4;
+    static constexpr int SLOTS = W * 8 * 4;
     static constexpr int MISC = 512;
     static constexpr int OFF_HIST = 0;
     static constexpr int OFF_UNION = OFF_HIST + HIST;
@@ -88,30 +92,30 @@ struct EncLayout {
 // misc area (uint32 index)
 enum {
     M_MSG = 0, M_NS = 1, M_K = 2 /*2*/, M_LAST = 4 /*2*/, M_FIRST = 6 /*2*/, M_SELA = 8 /*8*/,
-    M_SELB = 16 /*8*/, M_DANG = 24 /*2*/, M_STATUS = 26, M_MAP = 32 /*16*/, M_ENT = 64 /*16 doubles*/,
-    M_BASE = 96 /*u64*/, M_P = 100 /*2*/
+    M_SELB = 16 /*8*/, M_STATUS = 26, M_MAP = 32 /*16*/, M_ENT = 64 /*16 doubles*/, M_BASE = 96 /*u64*/
 };
+// per-wave slots (uint32, 8 per wave): 0,1 max(last run start+1); 2,3 chunk-start count;
+// 4 chunk bit 0 of the wave's first group (stream 1 in bit 16); 5,6 max(last chunk start+1)
 
 __device__ __forceinline__ uint32_t popc(uint32_t x) { return (uint32_t)__builtin_popcount(x); }
 __device__ __forceinline__ uint32_t hibit(uint32_t x) { return 31u - (uint32_t)__builtin_clz(x); }
 __device__ __forceinline__ uint32_t lobit(uint32_t x) { return (uint32_t)__builtin_ctz(x); }
-__device__ __forceinline__ uint32_t byte_of(uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3, uint32_t j) {
-    const uint32_t w = j < 4 ? s0 : j < 8 ? s1 : j < 12 ? s2 : s3;
-    return (w >> (8 * (j & 3))) & 0xffu;
+__device__ __forceinline__ uint32_t umax(uint32_t a, uint32_t b) { return a > b ? a : b; }
+__device__ __forceinline__ uint32_t dword_of(const uint4 &d, uint32_t q) {
+    return q == 0 ? d.x : q == 1 ? d.y : q == 2 ? d.z : d.w;
+}
+__device__ __forceinline__ uint32_t shfl_up1(uint32_t x) { return (uint32_t)__shfl_up((int)x, 1); }
+__device__ __forceinline__ uint32_t shfl_down1(uint32_t x) { return (uint32_t)__shfl_down((int)x, 1); }
+__device__ __forceinline__ uint32_t rdlane(uint32_t x, int l) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)x, l);
 }
 
-// Uniform per-message stream description, read into SGPRs.
+// Uniform per-message stream description.
 struct StreamDesc {
     uint32_t ns;
     uint32_t k[2];
     uint32_t last[2], first[2];
     uint32_t selA[2][4], selB[2][4];
-};
-
-// Per-group, per-stream RLE analysis shared by the count pass and the emit pass.
-struct GS {
-    uint32_t s[4];
-    uint32_t L, gpos, mask, chunk, cs_enc;
 };
 
 template <int WS, int TEAM, int G, int MODE>
@@ -121,10 +125,11 @@ __global__ __launch_bounds__(TEAM) void tdt_encode_kernel(EncodeArgs a) {
     constexpr int WPG = Lay::WPG;
     __shared__ __attribute__((aligned(16))) uint8_t smem[Lay::BYTES];
     uint32_t *hist = reinterpret_cast<uint32_t *>(smem + Lay::OFF_HIST);
-    uint8_t *uni = smem + Lay::OFF_UNION;
     uint32_t *slots = reinterpret_cast<uint32_t *>(smem + Lay::OFF_SLOTS);
     uint32_t *misc = reinterpret_cast<uint32_t *>(smem + Lay::OFF_MISC);
     const int tid = threadIdx.x;
+    const int lane = lane_id();
+    const int wv = tid >> 6;
 
     if (tid == 0) misc[M_MSG] = atomicAdd(a.ticket, 1u);
     team_sync<W>();
@@ -176,37 +181,49 @@ __global__ __launch_bounds__(TEAM) void tdt_encode_kernel(EncodeArgs a) {
     const uint32_t n32 = (uint32_t)n;
     const uint32_t wc = n32 / WS;
     const uint32_t ngroups = (n32 + 15) / 16;
-    const uint32_t nrounds = (ngroups + TEAM - 1) / TEAM;
-    const bool resident = nrounds <= (uint32_t)G;
+    const uint32_t RW = (ngroups + TEAM - 1) / TEAM;  // rounds per wave
+    const bool resident = RW <= (uint32_t)G;
     const bool al16 = ((uintptr_t)base & 15) == 0;
+    const uint32_t gw0 = (uint32_t)wv * RW * 64;  // first group of this wave
 
-    auto load_group = [&](uint32_t r) __attribute__((always_inline)) -> uint4 {
-        const uint32_t g = r * TEAM + tid;
+    auto vbytes = [&](uint32_t g) __attribute__((always_inline)) -> uint32_t {
         const int64_t vb64 = (int64_t)n32 - 16 * (int64_t)g;
-        const int vb = vb64 >= 16 ? 16 : (vb64 <= 0 ? 0 : (int)vb64);
+        return vb64 >= 16 ? 16u : (vb64 <= 0 ? 0u : (uint32_t)vb64);
+    };
+    auto load_group = [&](uint32_t r) __attribute__((always_inline)) -> uint4 {
+        const uint32_t g = gw0 + r * 64 + lane;
+        const uint32_t vb = vbytes(g);
         if (vb == 16 && al16) return *reinterpret_cast<const uint4 *>(base + 16ull * g);
-        if (vb <= 0) return make_uint4(0, 0, 0, 0);
-        return ld16_any(base + 16ull * g, vb);
+        if (vb == 0) return make_uint4(0, 0, 0, 0);
+        return ld16_any(base + 16ull * g, (int)vb);
     };
 
-    // Resident messages keep their G rounds in VGPRs; the round loop ROTATES the array (all
-    // indices compile-time constant) instead of indexing it with the runtime round number,
-    // which would push it to scratch.
+    // Resident messages keep their RW <= G rounds in VGPRs.  The round loop ROTATES the
+    // arrays (compile-time indices only) instead of indexing them with the round number,
+    // which would push them to scratch.
     uint4 dres[G];
+    uint32_t cres[G];  // chunk-start masks of both streams (stream 1 in the high half)
 #pragma unroll
-    for (int r = 0; r < G; ++r)
-        dres[r] = (resident && (uint32_t)r < nrounds) ? load_group(r) : make_uint4(0, 0, 0, 0);
+    for (int r = 0; r < G; ++r) {
+        dres[r] = (resident && (uint32_t)r < RW) ? load_group(r) : make_uint4(0, 0, 0, 0);
+        cres[r] = 0;
+    }
     auto rotate = [&]() __attribute__((always_inline)) {
         const uint4 t = dres[0];
+        const uint32_t c = cres[0];
 #pragma unroll
-        for (int q = 0; q < G - 1; ++q) dres[q] = dres[q + 1];
+        for (int q = 0; q < G - 1; ++q) {
+            dres[q] = dres[q + 1];
+            cres[q] = cres[q + 1];
+        }
         dres[G - 1] = t;
+        cres[G - 1] = c;
     };
-    // body(r, data) for every round r < nrounds, in order
+    // body(r, data, chunk_slot&) for every round r < RW of this wave, in order
     auto for_rounds = [&](auto &&body) __attribute__((always_inline)) {
-        const uint32_t iters = resident ? (uint32_t)G : nrounds;
+        const uint32_t iters = resident ? (uint32_t)G : RW;
         for (uint32_t r = 0; r < iters; ++r) {
-            if (r < nrounds) body(r, resident ? dres[0] : load_group(r));
+            if (r < RW) body(r, resident ? dres[0] : load_group(r), cres[0]);
             if (resident) rotate();
         }
     };
@@ -234,33 +251,34 @@ __global__ __launch_bounds__(TEAM) void tdt_encode_kernel(EncodeArgs a) {
             return;
         }
     } else {
-        // histograms: extract_features :441-446 over every word (full sample)
+        // histograms: extract_features :441-446 over every word (full sample).  Zero bytes
+        // (dominant in float tensors) are counted in registers and added once per wave.
         for (int i = tid; i < WS * 256; i += TEAM) hist[i] = 0;
         team_sync<W>();
-        const int lane = lane_id();
-        for_rounds([&](uint32_t r, const uint4 d) __attribute__((always_inline)) {
-            const uint32_t g = r * TEAM + tid;
-            const int64_t vb64 = (int64_t)n32 - 16 * (int64_t)g;
-            const int vb = vb64 >= 16 ? 16 : (vb64 <= 0 ? 0 : (int)vb64);
+        uint32_t zc[WS];
+#pragma unroll
+        for (int b = 0; b < WS; ++b) zc[b] = 0;
+        for_rounds([&](uint32_t r, const uint4 d, uint32_t &) __attribute__((always_inline)) {
+            const uint32_t vb = vbytes(gw0 + r * 64 + lane);
             const uint32_t dw[4] = {d.x, d.y, d.z, d.w};
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
-                const bool valid = i < vb;
                 const uint32_t v = (dw[i >> 2] >> (8 * (i & 3))) & 0xffu;
-                const uint64_t act = __ballot(valid);
-                if (act == 0) continue;
-                const int leader = __builtin_ctzll(act);
-                const uint32_t lv = (uint32_t)__builtin_amdgcn_readlane((int)v, leader);
-                const uint64_t same = __ballot(valid && v == lv);
-                uint32_t *hb = hist + (i % WS) * 256;
-                if (lane == leader) atomicAdd(hb + lv, (uint32_t)__builtin_popcountll(same));
-                if (valid && v != lv) atomicAdd(hb + v, 1u);
+                if ((uint32_t)i < vb) {
+                    if (v == 0) zc[i % WS]++;
+                    else atomicAdd(hist + (i % WS) * 256 + v, 1u);
+                }
             }
         });
+#pragma unroll
+        for (int b = 0; b < WS; ++b) {
+            const uint32_t t = wave_reduce<OpAdd>(zc[b]);
+            if (lane == 0 && t) atomicAdd(hist + b * 256, t);
+        }
         team_sync<W>();
 
         // entropies: calculate_entropy :470-480, TB byte positions per batch
-        double *terms = reinterpret_cast<double *>(uni);
+        double *terms = reinterpret_cast<double *>(smem + Lay::OFF_UNION);
         const double total = (double)wc;
         for (int q0 = 0; q0 < WS; q0 += Lay::TB) {
             for (int i = tid; i < Lay::TB * 256; i += TEAM) {
@@ -283,9 +301,12 @@ __global__ __launch_bounds__(TEAM) void tdt_encode_kernel(EncodeArgs a) {
             if (tid < Lay::TB && q0 + tid < WS) {
                 const int b = q0 + tid;
                 double e = 0.0;
+#pragma unroll 8
                 for (int v = 0; v < 256; ++v) {
                     const uint32_t c = hist[b * 256 + v];
-                    if (c) e = __builtin_fma(-terms[2 * (tid * 256 + v)], terms[2 * (tid * 256 + v) + 1], e);
+                    const double p = terms[2 * (tid * 256 + v)];
+                    const double L = terms[2 * (tid * 256 + v) + 1];
+                    e = c ? __builtin_fma(-p, L, e) : e;
                 }
                 reinterpret_cast<double *>(misc + M_ENT)[b] = e;
             }
@@ -361,171 +382,147 @@ __global__ __launch_bounds__(TEAM) void tdt_encode_kernel(EncodeArgs a) {
                 sd.selB[c][q] = __builtin_amdgcn_readfirstlane(misc[M_SELB + 4 * c + q]);
             }
         }
+        if (sd.ns < 2) sd.k[1] = 0;  // stream 1 absent: every group has L = 0 for it
+        // the byte of the previous group that precedes stream c's first byte of a group
+        uint32_t pq[2], pb[2];
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            const uint32_t i = 16 - WS + sd.last[c];
+            pq[c] = i >> 2;
+            pb[c] = 8 * (i & 3);
+        }
 
-        // Per-group analysis of stream c for round r (shared by both passes).
-        auto analyze = [&](const uint4 &d, uint32_t g, int c, uint32_t prevb) __attribute__((always_inline)) -> GS {
-            GS x;
-            const int64_t vb64 = (int64_t)n32 - 16 * (int64_t)g;
-            const uint32_t vb = vb64 >= 16 ? 16u : (vb64 <= 0 ? 0u : (uint32_t)vb64);
-            x.L = (vb / WS) * sd.k[c];
-            x.gpos = g * WPG * sd.k[c];
+        auto gather = [&](const uint4 &d, int c, uint32_t (&s)[4]) __attribute__((always_inline)) {
 #pragma unroll
             for (int q = 0; q < 4; ++q)
-                x.s[q] = __builtin_amdgcn_perm(d.y, d.x, sd.selA[c][q]) |
-                         __builtin_amdgcn_perm(d.w, d.z, sd.selB[c][q]);
-            uint32_t m = neq_prev_mask4(x.s[0], prevb << 24) | (neq_prev_mask4(x.s[1], x.s[0]) << 4) |
-                         (neq_prev_mask4(x.s[2], x.s[1]) << 8) | (neq_prev_mask4(x.s[3], x.s[2]) << 12);
-            if (g == 0) m |= 1u;
-            x.mask = x.L ? (m & ((1u << x.L) - 1u)) : 0u;
-            x.chunk = 0;
-            x.cs_enc = 0;
-            return x;
+                s[q] = __builtin_amdgcn_perm(d.y, d.x, sd.selA[c][q]) | __builtin_amdgcn_perm(d.w, d.z, sd.selB[c][q]);
         };
-
-        // carried run start + 255-cap boundary → chunk-start mask (simple_rle_compress :567-575)
-        auto chunks = [&](GS &x) __attribute__((always_inline)) {
-            uint32_t cap = 0;
-            if (x.L && !(x.mask & 1u) && x.cs_enc) {
-                const uint32_t cs = x.cs_enc - 1;
-                const uint32_t fs = x.mask ? lobit(x.mask) : x.L;
-                const uint32_t kk = (x.gpos - cs + 254u) / 255u;
-                const uint32_t cpos = cs + 255u * kk;
-                if (cpos < x.gpos + fs) cap = 1u << (cpos - x.gpos);
-            }
-            x.chunk = x.mask | cap;
-        };
-
-        uint32_t carry_max[2] = {0, 0};
-        uint32_t carry_P[2] = {0, 0};
-        uint32_t scan_par = 0;
-
-        // one round of the count pass (EMIT=false) or the emit pass (EMIT=true)
-        auto round = [&](uint32_t r, const uint4 d, auto emit_tag, uint64_t out_base, const uint32_t *sdata,
-                         uint64_t E) __attribute__((always_inline)) {
-            constexpr bool EMIT = decltype(emit_tag)::value;
-            const uint32_t g = r * TEAM + tid;
-            const bool last_group = 16ull * (g + 1) >= n;
-            uint32_t prevb[2] = {0, 0}, nextb[2] = {0, 0};
+        // run-start masks of both streams for round r (stream 1 in bits 16..31)
+        auto run_masks = [&](uint32_t r, const uint4 &d) __attribute__((always_inline)) -> uint32_t {
+            const uint32_t g = gw0 + r * 64 + lane;
+            const uint32_t nvw = vbytes(g) / WS;
+            uint32_t out = 0;
 #pragma unroll
             for (int c = 0; c < 2; ++c) {
-                if ((uint32_t)c < sd.ns && sd.k[c]) {
-                    if (g > 0 && 16ull * g < n) prevb[c] = base[16ull * g - WS + sd.last[c]];
-                    if (EMIT && !last_group) nextb[c] = base[16ull * (g + 1) + sd.first[c]];
-                }
+                if (sd.k[c] == 0) continue;  // uniform
+                const uint32_t L = nvw * sd.k[c];
+                // previous group's last word from lane-1; lane 0 reads it from memory
+                const uint32_t pw = shfl_up1(dword_of(d, pq[c]));
+                uint32_t prevb = (pw >> pb[c]) & 0xffu;
+                if (lane == 0 && g > 0 && L) prevb = base[16ull * g - WS + sd.last[c]];
+                uint32_t s[4];
+                gather(d, c, s);
+                uint32_t m = neq_prev_mask4(s[0], prevb << 24) | (neq_prev_mask4(s[1], s[0]) << 4) |
+                             (neq_prev_mask4(s[2], s[1]) << 8) | (neq_prev_mask4(s[3], s[2]) << 12);
+                if (g == 0) m |= 1u;
+                m = L ? (m & ((1u << L) - 1u)) : 0u;
+                out |= m << (16 * c);
             }
-            GS x[2];
-#pragma unroll
-            for (int c = 0; c < 2; ++c) x[c] = analyze(d, g, c, prevb[c]);
-            if (sd.ns < 2) {
-                x[1].L = 0;
-                x[1].mask = 0;
-            }
-            // max-scan of (last run start + 1)
-            uint32_t mv[2], mt[2];
-#pragma unroll
-            for (int c = 0; c < 2; ++c) mv[c] = x[c].mask ? x[c].gpos + hibit(x[c].mask) + 1u : 0u;
-            team_excl_scan<W, 2, OpMax>(mv, mt, slots + (scan_par & 1) * W * 4);
-            ++scan_par;
-            uint32_t sv[4], st[4];
+            return out;
+        };
+        // chunk-start masks for round r given run-start masks m and the carried maximum of
+        // (last run start + 1) before the round; advances the carry (rm).
+        auto chunk_masks = [&](uint32_t r, uint32_t m, uint32_t (&rm)[2]) __attribute__((always_inline)) -> uint32_t {
+            const uint32_t g = gw0 + r * 64 + lane;
+            const uint32_t nvw = vbytes(g) / WS;
+            uint32_t chunkp = 0;
 #pragma unroll
             for (int c = 0; c < 2; ++c) {
-                x[c].cs_enc = mv[c] > carry_max[c] ? mv[c] : carry_max[c];
-                carry_max[c] = mt[c] > carry_max[c] ? mt[c] : carry_max[c];
-                chunks(x[c]);
-                sv[c] = popc(x[c].chunk);
+                if (sd.k[c] == 0) continue;
+                const uint32_t mc = (m >> (16 * c)) & 0xffffu;
+                const uint32_t L = nvw * sd.k[c];
+                const uint32_t gpos = g * WPG * sd.k[c];
+                const uint32_t mv = mc ? gpos + hibit(mc) + 1u : 0u;
+                const uint32_t inc = wave_incl_scan<OpMax>(mv);
+                uint32_t cs_enc = wave_shift_up1(inc);
+                cs_enc = umax(cs_enc, rm[c]);
+                rm[c] = umax(rm[c], rdlane(inc, 63));
+                // 255-cap inside the carried run (simple_rle_compress :568)
+                uint32_t cap = 0;
+                if (L && !(mc & 1u) && cs_enc) {
+                    const uint32_t cs = cs_enc - 1;
+                    const uint32_t fs = mc ? lobit(mc) : L;
+                    const uint32_t cpos = cs + 255u * ((gpos - cs + 254u) / 255u);
+                    if (cpos < gpos + fs) cap = 1u << (cpos - gpos);
+                }
+                chunkp |= (mc | cap) << (16 * c);
             }
-            uint32_t endm[2] = {0, 0};
-            if (EMIT) {
-#pragma unroll
-                for (int c = 0; c < 2; ++c) {
-                    if (x[c].L) {
-                        bool lend = last_group;
-                        if (!lend) {
-                            const uint32_t lb = byte_of(x[c].s[0], x[c].s[1], x[c].s[2], x[c].s[3], x[c].L - 1);
-                            const uint32_t rs = x[c].mask ? x[c].gpos + hibit(x[c].mask) : x[c].cs_enc - 1;
-                            lend = (nextb[c] != lb) || ((x[c].gpos + x[c].L - rs) % 255u == 0);
-                        }
-                        endm[c] = ((x[c].chunk >> 1) | ((uint32_t)lend << (x[c].L - 1))) & ((1u << x[c].L) - 1u);
-                    }
-                }
-                if (tid == 0) {
-                    misc[M_DANG + 0] = (x[0].L && !(x[0].chunk & 1u)) ? 1u : 0u;
-                    misc[M_DANG + 1] = (x[1].L && !(x[1].chunk & 1u)) ? 1u : 0u;
-                }
-            }
-            sv[2] = popc(endm[0]);
-            sv[3] = popc(endm[1]);
-            team_excl_scan<W, 4, OpAdd>(sv, st, slots + (scan_par & 1) * W * 4);
-            ++scan_par;
-            if (EMIT) {
-                uint32_t k0[2], ra[2];
-#pragma unroll
-                for (int c = 0; c < 2; ++c) {
-                    k0[c] = carry_P[c] - misc[M_DANG + c];
-                    const uintptr_t dst = (uintptr_t)a.out + out_base + sdata[c] + 2ull * k0[c];
-                    ra[c] = (uint32_t)(dst & 15);
-                }
-#pragma unroll
-                for (int c = 0; c < 2; ++c) {
-                    uint32_t em = endm[c];
-                    const uint32_t pb = carry_P[c] + sv[c];
-                    const uint32_t rbase = Lay::OFF_UNION + c * Lay::REGION + ra[c];
-                    while (em) {
-                        const uint32_t j = lobit(em);
-                        em &= em - 1u;
-                        const uint32_t below = x[c].chunk & ((2u << j) - 1u);
-                        uint32_t cnt, idx;
-                        if (below) {
-                            cnt = j - hibit(below) + 1u;
-                            idx = pb + popc(below) - 1u;
-                        } else {
-                            const uint32_t cs = x[c].cs_enc - 1u;
-                            const uint32_t st0 = cs + 255u * ((x[c].gpos + j - cs) / 255u);
-                            cnt = x[c].gpos + j - st0 + 1u;
-                            idx = pb - 1u;
-                        }
-                        const uint32_t val = byte_of(x[c].s[0], x[c].s[1], x[c].s[2], x[c].s[3], j);
-                        const uint32_t rel = idx - k0[c];
-                        if (rel < st[2 + c]) {  // always true for a consistent round
-                            smem[rbase + 2u * rel] = (uint8_t)cnt;
-                            smem[rbase + 2u * rel + 1u] = (uint8_t)val;
-                        } else {
-                            atomicOr(a.errflags, 2u);
-                        }
-                    }
-                }
-                team_sync<W>();
-                // flush both regions: LDS (congruent mod 16 with the destination) → global
-#pragma unroll
-                for (int c = 0; c < 2; ++c) {
-                    uint32_t len = 2u * st[2 + c];
-                    if (len && sdata[c] + 2ull * k0[c] + len > E) {  // never for a consistent round
-                        if (tid == 0) atomicOr(a.errflags, 4u);
-                        len = 0;
-                    }
-                    if (len) {
-                        uint8_t *dst = a.out + out_base + sdata[c] + 2ull * k0[c];
-                        const uint32_t sb = Lay::OFF_UNION + c * Lay::REGION + ra[c];
-                        const uint32_t head0 = (16u - ra[c]) & 15u;
-                        const uint32_t head = head0 < len ? head0 : len;
-                        const uint32_t body = (len - head) & ~15u;
-                        if ((uint32_t)tid < head) dst[tid] = smem[sb + tid];
-                        for (uint32_t k = tid; k < body / 16; k += TEAM)
-                            *reinterpret_cast<uint4 *>(dst + head + 16 * k) =
-                                *reinterpret_cast<const uint4 *>(smem + sb + head + 16 * k);
-                        const uint32_t tail = len - head - body;
-                        if ((uint32_t)tid < tail) dst[head + body + tid] = smem[sb + head + body + tid];
-                    }
-                }
-            }
-#pragma unroll
-            for (int c = 0; c < 2; ++c) carry_P[c] += st[c];
+            return chunkp;
         };
 
-        // ---------------------------------------------------------- pass A: count pairs
-        const uint32_t nosd[2] = {0, 0};
-        for_rounds([&](uint32_t r, const uint4 d) __attribute__((always_inline)) { round(r, d, std::false_type{}, 0, nosd, 0); });
-        const uint32_t P0 = carry_P[0], P1 = sd.ns > 1 ? carry_P[1] : 0;
+        // ---------------------------------------------------------- pass A1: run starts
+        uint32_t wmax[2] = {0, 0};
+        for_rounds([&](uint32_t r, const uint4 d, uint32_t &cm) __attribute__((always_inline)) {
+            const uint32_t g = gw0 + r * 64 + lane;
+            const uint32_t m = run_masks(r, d);
+            cm = m;  // kept for A2 (resident messages)
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                if (sd.k[c] == 0) continue;
+                const uint32_t mc = (m >> (16 * c)) & 0xffffu;
+                const uint32_t gpos = g * WPG * sd.k[c];
+                const uint32_t mv = mc ? gpos + hibit(mc) + 1u : 0u;
+                wmax[c] = umax(wmax[c], wave_reduce<OpMax>(mv));
+            }
+        });
+        if (lane == 0) {
+            slots[wv * 8 + 0] = wmax[0];
+            slots[wv * 8 + 1] = wmax[1];
+        }
+        team_sync<W>();
+        uint32_t rin[2] = {0, 0};  // max (run start + 1) before this wave
+#pragma unroll
+        for (int ww = 0; ww < W; ++ww)
+            if (ww < wv) {
+                rin[0] = umax(rin[0], slots[ww * 8 + 0]);
+                rin[1] = umax(rin[1], slots[ww * 8 + 1]);
+            }
+        rin[0] = __builtin_amdgcn_readfirstlane(rin[0]);
+        rin[1] = __builtin_amdgcn_readfirstlane(rin[1]);
+
+        // ---------------------------------------------------------- pass A2: chunk starts
+        uint32_t rm[2] = {rin[0], rin[1]};
+        uint32_t psum[2] = {0, 0}, cmaxw[2] = {0, 0};
+        uint32_t fb0 = 0;  // chunk bit 0 of this wave's first group (stream 1 in bit 16)
+        for_rounds([&](uint32_t r, const uint4 d, uint32_t &cm) __attribute__((always_inline)) {
+            const uint32_t g = gw0 + r * 64 + lane;
+            const uint32_t m = resident ? cm : run_masks(r, d);
+            const uint32_t chunkp = chunk_masks(r, m, rm);
+            if (resident) cm = chunkp;  // kept for pass B
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                if (sd.k[c] == 0) continue;
+                const uint32_t ch = (chunkp >> (16 * c)) & 0xffffu;
+                const uint32_t gpos = g * WPG * sd.k[c];
+                psum[c] += wave_reduce<OpAdd>(popc(ch));
+                cmaxw[c] = umax(cmaxw[c], wave_reduce<OpMax>(ch ? gpos + hibit(ch) + 1u : 0u));
+            }
+            if (r == 0) fb0 = rdlane(chunkp, 0) & 0x10001u;
+        });
+        if (lane == 0) {
+            slots[wv * 8 + 2] = psum[0];
+            slots[wv * 8 + 3] = psum[1];
+            slots[wv * 8 + 4] = fb0;
+            slots[wv * 8 + 5] = cmaxw[0];
+            slots[wv * 8 + 6] = cmaxw[1];
+        }
+        team_sync<W>();
+        uint32_t pin[2] = {0, 0}, ptot[2] = {0, 0}, cin[2] = {0, 0};
+#pragma unroll
+        for (int ww = 0; ww < W; ++ww) {
+            const uint32_t s0 = slots[ww * 8 + 2], s1 = slots[ww * 8 + 3];
+            if (ww < wv) {
+                pin[0] += s0;
+                pin[1] += s1;
+                cin[0] = umax(cin[0], slots[ww * 8 + 5]);
+                cin[1] = umax(cin[1], slots[ww * 8 + 6]);
+            }
+            ptot[0] += s0;
+            ptot[1] += s1;
+        }
+        const uint32_t nfb = __builtin_amdgcn_readfirstlane((wv + 1 < W) ? slots[(wv + 1) * 8 + 4] : 0u);
+        const uint32_t P0 = __builtin_amdgcn_readfirstlane(ptot[0]);
+        const uint32_t P1 = sd.ns > 1 ? __builtin_amdgcn_readfirstlane(ptot[1]) : 0u;
         const uint32_t hdr = 20 + 4 * WS;
         const uint64_t E = hdr + (4 + 2ull * P0) + (sd.ns > 1 ? 4 + 2ull * P1 : 0);
         if (tid == 0) {
@@ -561,10 +558,109 @@ __global__ __launch_bounds__(TEAM) void tdt_encode_kernel(EncodeArgs a) {
                 dst[sdata[c] - 4 + (tid & 3)] = (uint8_t)(len >> sh);
             }
         }
+
         // ---------------------------------------------------------- pass B: emit pairs
-        carry_max[0] = carry_max[1] = 0;
-        carry_P[0] = carry_P[1] = 0;
-        for_rounds([&](uint32_t r, const uint4 d) __attribute__((always_inline)) { round(r, d, std::true_type{}, ob, sdata, E); });
+        // Everything below is wave-local: per-wave LDS staging, no workgroup barrier.
+        const uint32_t wst = Lay::OFF_UNION + wv * Lay::WSTAGE;
+        uint32_t pr[2] = {(uint32_t)__builtin_amdgcn_readfirstlane(pin[0]), (uint32_t)__builtin_amdgcn_readfirstlane(pin[1])};
+        uint32_t cmc[2] = {(uint32_t)__builtin_amdgcn_readfirstlane(cin[0]), (uint32_t)__builtin_amdgcn_readfirstlane(cin[1])};
+        uint32_t rmB[2] = {rin[0], rin[1]};
+        for_rounds([&](uint32_t r, const uint4 d, uint32_t &cm) __attribute__((always_inline)) {
+            const uint32_t g = gw0 + r * 64 + lane;
+            const uint32_t nvw = vbytes(g) / WS;
+            const bool last_group = 16ull * (g + 1) >= n;
+            const uint32_t chunkp = resident ? cm : chunk_masks(r, run_masks(r, d), rmB);
+            const uint32_t nxt = shfl_down1(chunkp);  // next group's chunk starts (lanes < 63)
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                if (sd.k[c] == 0) continue;  // uniform
+                const uint32_t L = nvw * sd.k[c];
+                const uint32_t gpos = g * WPG * sd.k[c];
+                const uint32_t ch = (chunkp >> (16 * c)) & 0xffffu;
+                // last chunk start (+1) before this group: wave max-scan + carry
+                const uint32_t lc = ch ? gpos + hibit(ch) + 1u : 0u;
+                const uint32_t cinc = wave_incl_scan<OpMax>(lc);
+                uint32_t ccs = wave_shift_up1(cinc);
+                ccs = umax(ccs, cmc[c]);
+                const uint32_t ctot = rdlane(cinc, 63);
+                // chunk starts before this group → pair indices
+                const uint32_t pc = popc(ch);
+                const uint32_t pinc = wave_incl_scan<OpAdd>(pc);
+                const uint32_t pbase = pr[c] + pinc - pc;
+                const uint32_t rtot = rdlane(pinc, 63);
+                uint32_t s[4];
+                gather(d, c, s);
+                // chunk END at slot L-1 iff the next stream byte starts a chunk
+                uint32_t e = 0;
+                if (L) {
+                    bool lend;
+                    if (last_group) {
+                        lend = true;
+                    } else if (lane < 63) {
+                        lend = (nxt >> (16 * c)) & 1u;
+                    } else if (r + 1 < RW) {
+                        // next group = lane 0 of this wave's next round: new run, or exactly
+                        // 255 bytes after the start of the chunk holding the last byte
+                        const uint32_t nb = base[16ull * (g + 1) + sd.first[c]];
+                        const uint32_t lb = (s[(L - 1) >> 2] >> (8 * ((L - 1) & 3))) & 0xffu;
+                        const uint32_t lcs = ch ? gpos + hibit(ch) : ccs - 1u;
+                        lend = (nb != lb) || (gpos + L - lcs == 255u);
+                    } else {
+                        lend = (nfb >> (16 * c)) & 1u;  // next wave's first group
+                    }
+                    e = ((ch >> 1) | ((uint32_t)lend << (L - 1))) & ((1u << L) - 1u);
+                }
+                // staging window of this wave-round: the pairs ending here, [k0, k0 + ends)
+                const uint32_t f0 = rdlane(ch, 0);
+                const uint32_t dang = (rdlane(L, 0) && !(f0 & 1u)) ? 1u : 0u;
+                const uint32_t k0 = pr[c] - dang;
+                const uint32_t ends = wave_reduce<OpAdd>(popc(e));
+                const uint64_t gdst = (uint64_t)(uintptr_t)dst + sdata[c] + 2ull * k0;
+                const uint32_t ra = (uint32_t)(gdst & 15);
+                const uint32_t rb = wst + c * Lay::WREGION + ra;
+                // start of the chunk holding slot 0, relative to gpos (<= 0)
+                int cst = (!(ch & 1u) && ccs) ? (int)(ccs - 1u) - (int)gpos : 0;
+                uint32_t nst = 0;  // chunk starts at slots <= j
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    const uint32_t isst = (ch >> j) & 1u;
+                    nst += isst;
+                    cst = isst ? j : cst;
+                    if ((e >> j) & 1u) {
+                        const uint32_t rel = pbase + nst - 1u - k0;
+                        const uint32_t cnt = (uint32_t)(j - cst + 1);
+                        const uint32_t val = (s[j >> 2] >> (8 * (j & 3))) & 0xffu;
+                        if (rel < ends) {
+                            smem[rb + 2 * rel] = (uint8_t)cnt;
+                            smem[rb + 2 * rel + 1] = (uint8_t)val;
+                        } else {
+                            atomicOr(a.errflags, 2u);
+                        }
+                    }
+                }
+                team_sync<1>();  // this wave's staging writes are visible to its other lanes
+                uint32_t len = 2u * ends;
+                if (len && sdata[c] + 2ull * k0 + len > E) {  // never for a consistent round
+                    if (lane == 0) atomicOr(a.errflags, 4u);
+                    len = 0;
+                }
+                if (len) {
+                    uint8_t *gd = dst + sdata[c] + 2ull * k0;
+                    const uint32_t head0 = (16u - ra) & 15u;
+                    const uint32_t head = head0 < len ? head0 : len;
+                    const uint32_t body = (len - head) & ~15u;
+                    if ((uint32_t)lane < head) gd[lane] = smem[rb + lane];
+                    for (uint32_t k = lane; k < body / 16; k += 64)
+                        *reinterpret_cast<uint4 *>(gd + head + 16 * k) =
+                            *reinterpret_cast<const uint4 *>(smem + rb + head + 16 * k);
+                    const uint32_t tail = len - head - body;
+                    if ((uint32_t)lane < tail) gd[head + body + lane] = smem[rb + head + body + lane];
+                }
+                team_sync<1>();
+                pr[c] += rtot;
+                cmc[c] = umax(cmc[c], ctot);
+            }
+        });
     }
 }
 
