@@ -414,4 +414,13 @@ const char *tdt_status_string(int status) {
     return "TDT: unknown status";
 }
 
+#if defined(PSY_PROF) && PSY_PROF
+// diagnostic builds only: read and clear the phase-cycle counters
+int tdt_prof_read(uint64_t *out32) {
+    if (hipMemcpyFromSymbol(out32, HIP_SYMBOL(psy::psy_prof), 32 * sizeof(uint64_t)) != hipSuccess) return TDT_E_HIP;
+    static const uint64_t zero[32] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(psy::psy_prof), zero, sizeof(zero)) != hipSuccess) return TDT_E_HIP;
+    return TDT_OK;
+}
+#endif
 }  // extern "C"

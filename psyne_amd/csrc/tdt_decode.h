@@ -63,6 +63,7 @@ __global__ __launch_bounds__(TEAM) void tdt_decode_kernel(DecodeArgs a) {
     uint32_t *slots = reinterpret_cast<uint32_t *>(smem + Lay::OFF_SLOTS);
     uint32_t *misc = reinterpret_cast<uint32_t *>(smem + Lay::OFF_MISC);
     const int tid = threadIdx.x;
+    PSY_PROF_BEGIN();
 
     if (tid == 0) misc[D_MSG] = atomicAdd(a.ticket, 1u);
     team_sync<W>();
@@ -197,6 +198,7 @@ __global__ __launch_bounds__(TEAM) void tdt_decode_kernel(DecodeArgs a) {
     team_sync<W>();
     const uint32_t st = __builtin_amdgcn_readfirstlane(misc[D_STATUS]);
     if (st != ST_OK) return;
+    PSY_PROF_MARK(8);
     const uint64_t ob = *reinterpret_cast<const uint64_t *>(misc + D_BASE);
     uint8_t *dst = a.out + ob;
     if (misc[D_UNCP]) {
@@ -279,6 +281,7 @@ __global__ __launch_bounds__(TEAM) void tdt_decode_kernel(DecodeArgs a) {
                 pidx += consumed;
                 if (consumed == 0) break;  // defensive: nothing starts below P1
             }
+            PSY_PROF_MARK(9);
             const uint64_t cover = pos < P1 ? pos : P1;
             if (tid == 0) {
                 misc[D_PIDX + r] = pidx;
@@ -311,8 +314,10 @@ __global__ __launch_bounds__(TEAM) void tdt_decode_kernel(DecodeArgs a) {
                 od[q] |= __builtin_amdgcn_perm(sb[1], sb[0], misc[D_SEL + 8 * r + q]) |
                          __builtin_amdgcn_perm(sb[3], sb[2], misc[D_SEL + 8 * r + 4 + q]);
             team_sync<W>();  // heads are rewritten by the next stream
+            PSY_PROF_MARK(10);
         }
         if (vb) st16_any(dst + 16ull * g, make_uint4(od[0], od[1], od[2], od[3]), (int)vb);
+        PSY_PROF_MARK(11);
     }
 }
 

@@ -16,6 +16,25 @@ constexpr int kWave = 64;
 
 __device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
 
+// Phase-cycle instrumentation for diagnostic builds only (-DPSY_PROF=1, tools/phase_prof.py):
+// wave-lane 0 accumulates s_memtime deltas per phase.  Compiled out of the product library.
+#if defined(PSY_PROF) && PSY_PROF
+__device__ unsigned long long psy_prof[32];
+#define PSY_PROF_BEGIN() uint64_t psy_pt_ = __builtin_amdgcn_s_memtime()
+#define PSY_PROF_MARK(i)                                                    \
+    do {                                                                    \
+        const uint64_t psy_t_ = __builtin_amdgcn_s_memtime();               \
+        if (lane_id() == 0) atomicAdd(&psy_prof[(i)], psy_t_ - psy_pt_);    \
+        psy_pt_ = psy_t_;                                                   \
+    } while (0)
+#elif defined(PSY_ASM_MARKS)
+#define PSY_PROF_BEGIN() ((void)0)
+#define PSY_PROF_MARK(i) asm volatile(";@@MARK " #i ::)
+#else
+#define PSY_PROF_BEGIN() ((void)0)
+#define PSY_PROF_MARK(i) ((void)0)
+#endif
+
 template <int CTRL, int ROWMASK = 0xf, int BANKMASK = 0xf>
 __device__ __forceinline__ uint32_t dpp_mov(uint32_t x) {
     // Lanes whose source is outside the row / disabled by ROWMASK receive 0 (the identity
@@ -45,6 +64,33 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
 __device__ __forceinline__ uint32_t wave_shift_up1(uint32_t x) {
     // lane l receives lane l-1's value, lane 0 receives 0
     return (uint32_t)__shfl_up((int)x, 1) * (lane_id() != 0);
+}
+
+// DPP wavefront shifts (GFX9 wave_shr:1 / wave_shl:1): lane l receives lane l-1 (resp.
+// l+1); the lane whose source lies outside the wave receives `old`.
+__device__ __forceinline__ uint32_t wave_shr1(uint32_t x, uint32_t old) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)x, 0x138, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint32_t wave_shl1(uint32_t x, uint32_t old) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)x, 0x130, 0xf, 0xf, false);
+}
+
+// Two independent u16 lanes per dword (v_pk_max_u16).
+typedef unsigned short psy_u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pk_max_u16(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(psy_u16x2, a),
+                                                                  __builtin_bit_cast(psy_u16x2, b)));
+}
+struct OpPkMax {
+    __device__ __forceinline__ static uint32_t f(uint32_t a, uint32_t b) { return pk_max_u16(a, b); }
+};
+
+// v_ffbh_u32 with its hardware semantics (count of leading zeros, 0xffffffff for 0), so the
+// compiler can neither add a zero fix-up nor treat 0 as poison.
+__device__ __forceinline__ uint32_t ffbh_u32(uint32_t x) {
+    uint32_t r;
+    asm("v_ffbh_u32 %0, %1" : "=v"(r) : "v"(x));
+    return r;
 }
 
 template <class Op>

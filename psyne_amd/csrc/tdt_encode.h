@@ -1,4 +1,4 @@
-// tdt_encode.h — batched TDT encode for CDNA4 (gfx950).
+// tdt_encode.h — batched TDT encode for CDNA4 (gfx950), v3.
 //
 // Restates include/psyne/protocol/tdt_compression.hpp (reference):
 //   encode                 :227-266  UNCP passthrough / TDT blob
@@ -12,24 +12,28 @@
 //   TDTEncodedData::serialize :81-117
 //
 // Work decomposition: one TEAM-thread workgroup per message, message ids
-// claimed through an atomic ticket.  A message is a sequence of 16-byte GROUPS.  Wave w of
-// the team owns the contiguous group range [w·RW·64, (w+1)·RW·64): round r of the wave is
-// one coalesced 1 KiB sweep (lane l ↔ group (w·RW + r)·64 + l).  Because every wave owns a
-// contiguous stretch of the byte streams, all per-round scans are wave-level DPP scans with
-// a uniform running carry; the team synchronises only to exchange wave carries (twice).
-// Messages of up to G rounds per wave stay in VGPRs across all passes (the round arrays are
-// rotated, never dynamically indexed), so HBM sees each payload byte once.
+// claimed through an atomic ticket.  A message is a sequence of 16-byte GROUPS.  Wave w owns
+// the contiguous group range [w·RW·64, (w+1)·RW·64); round r of the wave is one coalesced
+// 1 KiB sweep (lane l ↔ group (w·RW + r)·64 + l).  Messages of up to G rounds per wave stay
+// in VGPRs across all passes (the round arrays are rotated, never dynamically indexed).
 //
-// RLE in parallel, per group and stream c (L = words·k_c consecutive stream bytes):
-//   * run starts: SWAR byte compare against the byte before (neq_prev_mask4);
-//   * the 255 cap only splits the run carried INTO a group (a run starting inside a 16-byte
-//     group cannot reach 255 there), so a max-scan of the last run start gives every group
-//     its carried run start and at most one cap boundary → chunk-start mask (kept in VGPRs);
-//   * pairs are indexed by a sum-scan of chunk starts and emitted at chunk ENDS (the count
-//     is known locally), slot by slot with predicated LDS stores into a per-wave window that
-//     is congruent mod 16 with its destination, then flushed with 16-byte stores — the emit
-//     pass has no workgroup barrier at all.
-// Output offsets across messages come from a single-pass decoupled look-back.
+// Both streams of a group live in ONE 16-slot word — stream 0 in slots [0, L0), stream 1 in
+// [L0, 16) — transposed so that slot j = 4t + q is byte t of dword q: the byte before slot j
+// is then the same byte of the previous dword, and the run-start mask of all 16 slots costs
+// one v_perm plus a SWAR zero-byte test per dword.  Both streams' scans run as ONE packed
+// scan (two u16 halves: v_pk_max_u16 / carry-free adds).  Passes per message:
+//   H   histograms into replicated LDS bins (+ per-lane zero bins: no same-address atomics)
+//   E   entropies (exact fma chain) → mapping → slot selectors
+//   A1  run-start masks → each wave's last run start                   (team exchange 1)
+//   A2  chunk-start masks (255-cap of the carried run) → pair counts   (team exchange 2)
+//       → decoupled look-back on the blob size → header
+//   B   per wave and round, pairs are emitted branch-free: every slot writes (clz count,
+//       value) at its chunk's pair index (bcnt of the end mask) in ascending slot order, so a
+//       chunk's END slot writes last; one repair write per stream and lane rewrites the pair
+//       whose chunk began before the group (and any same-instruction collision).  The window
+//       is per wave, congruent (mod 16) with its destination, flushed with 16-byte stores.
+//       No workgroup barrier in pass B.
+// tools/emulate_encode.py restates this algorithm lane for lane (tests/test_emulator.py).
 #pragma once
 #include "tdt_device.h"
 #include "tdt_log2.h"
@@ -64,7 +68,7 @@ struct EncodeArgs {
     int32_t *map_out;
     uint64_t *lookback;
     uint32_t *ticket;
-    uint32_t *errflags;  // bit0 look-back timeout, bit1 staging index, bit2 flush bound
+    uint32_t *errflags;  // bit0 look-back timeout, bit2 flush bound
     uint64_t min_tensor;
     int32_t policy_on;  // bandwidth < threshold && cpu <= threshold (host-evaluated atomics)
 };
@@ -73,10 +77,15 @@ template <int WS, int TEAM>
 struct EncLayout {
     static constexpr int W = TEAM / 64;
     static constexpr int WPG = 16 / WS;  // words per 16-byte group
+    // histogram, per byte position: [64 per-lane zero bins][256 bins x HC copies] (uint32)
+    static constexpr int HC = 16 / WS;  // 16 KiB of copies whatever the word size
+    static constexpr int LOG_HC = HC == 1 ? 0 : HC == 2 ? 1 : HC == 4 ? 2 : HC == 8 ? 3 : 4;
+    static constexpr int PS = 64 + 256 * HC;
+    static constexpr int HIST = WS * PS * 4;
     static constexpr int TB = (TEAM >= 256) ? (WS < 4 ? WS : 4) : (WS < 2 ? WS : 2);
-    static constexpr int HIST = WS * 256 * 4;
-    static constexpr int WREGION = 2 * 64 * 16 + 16;  // one stream's pairs of one wave-round
-    static constexpr int WSTAGE = 2 * WREGION;        // both streams, per wave
+    // one stream's pairs of one wave-round: alignment pad + 1024 pairs + one garbage pair
+    static constexpr int WREGION = 16 + 2 * 64 * 16 + 16;
+    static constexpr int WSTAGE = 2 * WREGION;  // both streams, per wave
     static constexpr int STAGE = W * WSTAGE;
     static constexpr int TERMS = TB * 256 * 16;
     static constexpr int UNION = STAGE > TERMS ? STAGE : TERMS;
@@ -87,36 +96,37 @@ struct EncLayout {
     static constexpr int OFF_SLOTS = OFF_UNION + UNION;
     static constexpr int OFF_MISC = OFF_SLOTS + SLOTS;
     static constexpr int BYTES = OFF_MISC + MISC;
+    static_assert((1 << LOG_HC) == HC, "histogram copies");
 };
 
 // misc area (uint32 index)
 enum {
-    M_MSG = 0, M_NS = 1, M_K = 2 /*2*/, M_LAST = 4 /*2*/, M_FIRST = 6 /*2*/, M_SELA = 8 /*8*/,
-    M_SELB = 16 /*8*/, M_STATUS = 26, M_MAP = 32 /*16*/, M_ENT = 64 /*16 doubles*/, M_BASE = 96 /*u64*/
+    M_MSG = 0, M_NS = 1, M_L0 = 2, M_K0 = 3, M_K1 = 4, M_SELA = 8 /*4*/, M_SELB = 12 /*4*/, M_EDA = 16,
+    M_EDB = 17, M_STATUS = 26, M_MAP = 32 /*16*/, M_ENT = 64 /*16 doubles*/, M_BASE = 96 /*u64*/,
+    M_SB = 100 /*16*/
 };
 // per-wave slots (uint32, 8 per wave): 0,1 max(last run start+1); 2,3 chunk-start count;
-// 4 chunk bit 0 of the wave's first group (stream 1 in bit 16); 5,6 max(last chunk start+1)
+// 4 chunk bits of the wave's first group (combined slot layout)
 
 __device__ __forceinline__ uint32_t popc(uint32_t x) { return (uint32_t)__builtin_popcount(x); }
 __device__ __forceinline__ uint32_t hibit(uint32_t x) { return 31u - (uint32_t)__builtin_clz(x); }
 __device__ __forceinline__ uint32_t lobit(uint32_t x) { return (uint32_t)__builtin_ctz(x); }
 __device__ __forceinline__ uint32_t umax(uint32_t a, uint32_t b) { return a > b ? a : b; }
-__device__ __forceinline__ uint32_t dword_of(const uint4 &d, uint32_t q) {
-    return q == 0 ? d.x : q == 1 ? d.y : q == 2 ? d.z : d.w;
-}
-__device__ __forceinline__ uint32_t shfl_up1(uint32_t x) { return (uint32_t)__shfl_up((int)x, 1); }
-__device__ __forceinline__ uint32_t shfl_down1(uint32_t x) { return (uint32_t)__shfl_down((int)x, 1); }
 __device__ __forceinline__ uint32_t rdlane(uint32_t x, int l) {
     return (uint32_t)__builtin_amdgcn_readlane((int)x, l);
 }
-
-// Uniform per-message stream description.
-struct StreamDesc {
-    uint32_t ns;
-    uint32_t k[2];
-    uint32_t last[2], first[2];
-    uint32_t selA[2][4], selB[2][4];
-};
+__device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel) {
+    return __builtin_amdgcn_perm(hi, lo, sel);
+}
+// bit j of e duplicated into bits 2j and 2j+1 (16 → 32 bits)
+__device__ __forceinline__ uint32_t spread2(uint32_t e) {
+    uint32_t x = e & 0xffffu;
+    x = (x | (x << 8)) & 0x00ff00ffu;
+    x = (x | (x << 4)) & 0x0f0f0f0fu;
+    x = (x | (x << 2)) & 0x33333333u;
+    x = (x | (x << 1)) & 0x55555555u;
+    return x | (x << 1);
+}
 
 template <int WS, int TEAM, int G, int MODE>
 __global__ __launch_bounds__(TEAM) void tdt_encode_kernel(EncodeArgs a) {
@@ -124,17 +134,18 @@ __global__ __launch_bounds__(TEAM) void tdt_encode_kernel(EncodeArgs a) {
     constexpr int W = Lay::W;
     constexpr int WPG = Lay::WPG;
     __shared__ __attribute__((aligned(16))) uint8_t smem[Lay::BYTES];
-    uint32_t *hist = reinterpret_cast<uint32_t *>(smem + Lay::OFF_HIST);
     uint32_t *slots = reinterpret_cast<uint32_t *>(smem + Lay::OFF_SLOTS);
     uint32_t *misc = reinterpret_cast<uint32_t *>(smem + Lay::OFF_MISC);
     const int tid = threadIdx.x;
     const int lane = lane_id();
     const int wv = tid >> 6;
+    PSY_PROF_BEGIN();
 
     if (tid == 0) misc[M_MSG] = atomicAdd(a.ticket, 1u);
     team_sync<W>();
     const uint32_t msg = __builtin_amdgcn_readfirstlane(misc[M_MSG]);
     if (msg >= a.n_msgs) return;
+    PSY_PROF_MARK(0);
 
     const uint64_t off0 = a.in_off[msg];
     const uint64_t n = a.in_off[msg + 1] - off0;
@@ -190,22 +201,25 @@ __global__ __launch_bounds__(TEAM) void tdt_encode_kernel(EncodeArgs a) {
         const int64_t vb64 = (int64_t)n32 - 16 * (int64_t)g;
         return vb64 >= 16 ? 16u : (vb64 <= 0 ? 0u : (uint32_t)vb64);
     };
-    auto load_group = [&](uint32_t r) __attribute__((always_inline)) -> uint4 {
-        const uint32_t g = gw0 + r * 64 + lane;
+    auto load_group = [&](uint32_t g) __attribute__((always_inline)) -> uint4 {
         const uint32_t vb = vbytes(g);
         if (vb == 16 && al16) return *reinterpret_cast<const uint4 *>(base + 16ull * g);
         if (vb == 0) return make_uint4(0, 0, 0, 0);
         return ld16_any(base + 16ull * g, (int)vb);
+    };
+    // FULL round: its 64 groups all hold 16 message bytes (uniform)
+    auto full_round = [&](uint32_t r) __attribute__((always_inline)) -> bool {
+        return 16ull * (gw0 + r * 64 + 64) <= n;
     };
 
     // Resident messages keep their RW <= G rounds in VGPRs.  The round loop ROTATES the
     // arrays (compile-time indices only) instead of indexing them with the round number,
     // which would push them to scratch.
     uint4 dres[G];
-    uint32_t cres[G];  // chunk-start masks of both streams (stream 1 in the high half)
+    uint32_t cres[G];  // run-start masks (A1 → A2), then chunk-start masks (A2 → B)
 #pragma unroll
     for (int r = 0; r < G; ++r) {
-        dres[r] = (resident && (uint32_t)r < RW) ? load_group(r) : make_uint4(0, 0, 0, 0);
+        dres[r] = (resident && (uint32_t)r < RW) ? load_group(gw0 + r * 64 + lane) : make_uint4(0, 0, 0, 0);
         cres[r] = 0;
     }
     auto rotate = [&]() __attribute__((always_inline)) {
@@ -219,11 +233,11 @@ __global__ __launch_bounds__(TEAM) void tdt_encode_kernel(EncodeArgs a) {
         dres[G - 1] = t;
         cres[G - 1] = c;
     };
-    // body(r, data, chunk_slot&) for every round r < RW of this wave, in order
+    // body(r, data, cres&) for every round r < RW of this wave, in order
     auto for_rounds = [&](auto &&body) __attribute__((always_inline)) {
         const uint32_t iters = resident ? (uint32_t)G : RW;
         for (uint32_t r = 0; r < iters; ++r) {
-            if (r < RW) body(r, resident ? dres[0] : load_group(r), cres[0]);
+            if (r < RW) body(r, resident ? dres[0] : load_group(gw0 + r * 64 + lane), cres[0]);
             if (resident) rotate();
         }
     };
@@ -251,62 +265,82 @@ __global__ __launch_bounds__(TEAM) void tdt_encode_kernel(EncodeArgs a) {
             return;
         }
     } else {
-        // histograms: extract_features :441-446 over every word (full sample).  Zero bytes
-        // (dominant in float tensors) are counted in registers and added once per wave.
-        for (int i = tid; i < WS * 256; i += TEAM) hist[i] = 0;
+        // histograms: extract_features :441-446 over every word (full sample).  Byte value
+        // v at position p adds 1 to copy (lane mod HC) of bin v — or, for v = 0 (dominant in
+        // float tensors), to this lane's private zero bin — so one ds_add only sends two
+        // lanes to the same address when they hold the same nonzero value.
+        uint32_t *hist = reinterpret_cast<uint32_t *>(smem + Lay::OFF_HIST);
+        for (int i = tid; i < WS * Lay::PS; i += TEAM) hist[i] = 0;
         team_sync<W>();
-        uint32_t zc[WS];
-#pragma unroll
-        for (int b = 0; b < WS; ++b) zc[b] = 0;
-        for_rounds([&](uint32_t r, const uint4 d, uint32_t &) __attribute__((always_inline)) {
-            const uint32_t vb = vbytes(gw0 + r * 64 + lane);
+        const uint32_t zoff = (uint32_t)lane * 4u;
+        const uint32_t coff = (64u + ((uint32_t)lane & (Lay::HC - 1))) * 4u;
+        auto hist_group = [&](const uint4 &d, uint32_t vb, bool full) __attribute__((always_inline)) {
             const uint32_t dw[4] = {d.x, d.y, d.z, d.w};
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
                 const uint32_t v = (dw[i >> 2] >> (8 * (i & 3))) & 0xffu;
-                if ((uint32_t)i < vb) {
-                    if (v == 0) zc[i % WS]++;
-                    else atomicAdd(hist + (i % WS) * 256 + v, 1u);
-                }
+                const uint32_t ad = v ? (v << (Lay::LOG_HC + 2)) + coff : zoff;
+                if (full || (uint32_t)i < vb)
+                    atomicAdd(reinterpret_cast<uint32_t *>(smem + Lay::OFF_HIST + (i % WS) * Lay::PS * 4 + ad), 1u);
             }
+        };
+        for_rounds([&](uint32_t r, const uint4 d, uint32_t &) __attribute__((always_inline)) {
+            if (full_round(r)) hist_group(d, 16, true);
+            else hist_group(d, vbytes(gw0 + r * 64 + lane), false);
         });
-#pragma unroll
-        for (int b = 0; b < WS; ++b) {
-            const uint32_t t = wave_reduce<OpAdd>(zc[b]);
-            if (lane == 0 && t) atomicAdd(hist + b * 256, t);
+        team_sync<W>();
+        PSY_PROF_MARK(1);
+
+        // bin 0 = copies + the 64 per-lane zero bins
+        for (int b = wv; b < WS; b += W) {
+            const uint32_t z = wave_reduce<OpAdd>(hist[b * Lay::PS + lane]);
+            if (lane == 0) hist[b * Lay::PS + 64] += z;  // copy 0 of bin 0
         }
         team_sync<W>();
+        auto count = [&](int b, int v) __attribute__((always_inline)) -> uint32_t {
+            uint32_t c = 0;
+#pragma unroll
+            for (int k = 0; k < Lay::HC; ++k) c += hist[b * Lay::PS + 64 + v * Lay::HC + k];
+            return c;
+        };
 
-        // entropies: calculate_entropy :470-480, TB byte positions per batch
+        // entropies: calculate_entropy :470-480, TB byte positions per batch.  Each bin's
+        // (-prob, log2 prob) is computed in parallel (0, 0 for an empty bin, so the chain
+        // needs no select: fma(0, 0, e) == e for the non-negative running sum); one lane per
+        // position then runs the exact fma chain in bin order.
         double *terms = reinterpret_cast<double *>(smem + Lay::OFF_UNION);
         const double total = (double)wc;
         for (int q0 = 0; q0 < WS; q0 += Lay::TB) {
             for (int i = tid; i < Lay::TB * 256; i += TEAM) {
                 const int b = q0 + i / 256;
+                double np = 0.0, L = 0.0;
                 if (b < WS) {
-                    const uint32_t c = hist[b * 256 + (i & 255)];
+                    const uint32_t c = count(b, i & 255);
+                    if constexpr (MODE == MODE_ANALYZE) {
+                        if (a.hist_out) a.hist_out[((uint64_t)msg * WS + b) * 256 + (i & 255)] = c;
+                    }
                     if (c) {
-                        double prob, L;
+                        double prob;
                         {
 #pragma clang fp contract(off)
                             prob = (double)c / total;
                             L = psy_log2_glibc(prob, c_log2_tab, c_log2_tab2);
                         }
-                        terms[2 * i] = prob;
-                        terms[2 * i + 1] = L;
+                        np = -prob;
                     }
                 }
+                terms[2 * i] = np;
+                terms[2 * i + 1] = L;
             }
             team_sync<W>();
             if (tid < Lay::TB && q0 + tid < WS) {
                 const int b = q0 + tid;
+                const double2 *tp = reinterpret_cast<const double2 *>(terms) + tid * 256;
                 double e = 0.0;
-#pragma unroll 8
+#pragma unroll 16
                 for (int v = 0; v < 256; ++v) {
-                    const uint32_t c = hist[b * 256 + v];
-                    const double p = terms[2 * (tid * 256 + v)];
-                    const double L = terms[2 * (tid * 256 + v) + 1];
-                    e = c ? __builtin_fma(-p, L, e) : e;
+                    const double2 t = tp[v];
+                    e = __builtin_fma(t.x, t.y, e);
                 }
                 reinterpret_cast<double *>(misc + M_ENT)[b] = e;
             }
@@ -327,8 +361,6 @@ __global__ __launch_bounds__(TEAM) void tdt_encode_kernel(EncodeArgs a) {
         team_sync<W>();
         if constexpr (MODE == MODE_ANALYZE) {
             const uint64_t mb = (uint64_t)msg * WS;
-            if (a.hist_out)
-                for (int i = tid; i < WS * 256; i += TEAM) a.hist_out[mb * 256 + i] = hist[i];
             if (tid < WS) {
                 if (a.ent_out) a.ent_out[mb + tid] = reinterpret_cast<const double *>(misc + M_ENT)[tid];
                 if (a.map_out) a.map_out[mb + tid] = (int32_t)misc[M_MAP + tid];
@@ -339,132 +371,187 @@ __global__ __launch_bounds__(TEAM) void tdt_encode_kernel(EncodeArgs a) {
     }
 
     if constexpr (MODE != MODE_ANALYZE) {
-        // ------------------------------------------------ stream descriptors (thread 0)
-        if (tid == 0) {
-            uint32_t ns = 1;
-            for (int b = 0; b < WS; ++b)
-                if (misc[M_MAP + b]) ns = 2;
-            misc[M_NS] = ns;
-            for (int c = 0; c < 2; ++c) {
-                uint32_t pos[WS];
-                uint32_t k = 0;
-                for (int b = 0; b < WS; ++b)
-                    if (misc[M_MAP + b] == (uint32_t)c) pos[k++] = b;
-                misc[M_K + c] = k;
-                misc[M_LAST + c] = k ? pos[k - 1] : 0;
-                misc[M_FIRST + c] = k ? pos[0] : 0;
-                for (int q = 0; q < 4; ++q) {
-                    uint32_t A = 0x0c0c0c0cu, B = 0x0c0c0c0cu;
-                    for (int t = 0; t < 4; ++t) {
-                        const uint32_t j = 4 * q + t;
-                        if (k && j < WPG * k) {
-                            const uint32_t src = (j / k) * WS + pos[j % k];
-                            if (src < 8) A = (A & ~(0xffu << (8 * t))) | (src << (8 * t));
-                            else B = (B & ~(0xffu << (8 * t))) | ((src - 8) << (8 * t));
-                        }
-                    }
-                    misc[M_SELA + 4 * c + q] = A;
-                    misc[M_SELB + 4 * c + q] = B;
+        // ------------------------------------------------ slot layout (thread 0)
+        // separate_byte_streams :527-549: slot j < L0 is stream-0 byte j of the group
+        // (word j / k0, position pos0[j % k0]); slot j >= L0 is stream-1 byte j - L0.
+        // 16 threads: slot j's source byte in the group (no per-thread arrays: scratch-free)
+        if (tid < 16) {
+            uint32_t k[2] = {0, 0};
+            for (int b = 0; b < WS; ++b) k[misc[M_MAP + b]]++;
+            const uint32_t L0 = WPG * k[0];
+            const uint32_t j = (uint32_t)tid;
+            const uint32_t c = j < L0 ? 0u : 1u;
+            const uint32_t jj = c ? j - L0 : j;
+            const uint32_t rank = jj % k[c];
+            uint32_t b = 0, seen = 0;
+            for (int bb = 0; bb < WS; ++bb) {
+                if (misc[M_MAP + bb] == c) {
+                    if (seen == rank) b = bb;
+                    ++seen;
                 }
+            }
+            misc[M_SB + j] = (jj / k[c]) * WS + b;
+            if (j == 0) {
+                misc[M_NS] = k[1] ? 2u : 1u;
+                misc[M_L0] = L0;
+                misc[M_K0] = k[0];
+                misc[M_K1] = k[1];
             }
         }
         team_sync<W>();
-        StreamDesc sd;
-        sd.ns = __builtin_amdgcn_readfirstlane(misc[M_NS]);
+        if (tid < 5) {
+            const uint32_t L0 = misc[M_L0];
+            const bool two = misc[M_NS] == 2;
+            uint32_t A = 0x0c0c0c0cu, B = 0x0c0c0c0cu;
+            for (int t = 0; t < 4; ++t) {
+                // T[q] byte t = slot 4t + q; edges byte 0 stream-0 last slot, byte 1 slot 15,
+                // byte 2 stream-1 first slot
+                uint32_t s = 0xffu;
+                if (tid < 4) s = misc[M_SB + 4 * t + tid];
+                else if (t == 0 && L0 > 0) s = misc[M_SB + L0 - 1];
+                else if (t == 1) s = misc[M_SB + 15];
+                else if (t == 2 && two) s = misc[M_SB + L0];
+                if (s == 0xffu) continue;
+                if (s < 8) A = (A & ~(0xffu << (8 * t))) | (s << (8 * t));
+                else B = (B & ~(0xffu << (8 * t))) | ((s - 8) << (8 * t));
+            }
+            misc[tid < 4 ? M_SELA + tid : M_EDA] = A;
+            misc[tid < 4 ? M_SELB + tid : M_EDB] = B;
+        }
+        team_sync<W>();
+        const uint32_t ns = __builtin_amdgcn_readfirstlane(misc[M_NS]);
+        const bool ns2 = ns == 2;
+        const uint32_t L0 = __builtin_amdgcn_readfirstlane(misc[M_L0]);
+        const uint32_t k0 = __builtin_amdgcn_readfirstlane(misc[M_K0]);
+        const uint32_t k1 = __builtin_amdgcn_readfirstlane(misc[M_K1]);
+        const uint32_t Ls[2] = {L0, ns2 ? 16u - L0 : 0u};
+        const uint32_t lowL0 = L0 >= 16 ? 0xffffu : ((1u << L0) - 1u);
+        uint32_t selA[4], selB[4];
 #pragma unroll
-        for (int c = 0; c < 2; ++c) {
-            sd.k[c] = __builtin_amdgcn_readfirstlane(misc[M_K + c]);
-            sd.last[c] = __builtin_amdgcn_readfirstlane(misc[M_LAST + c]);
-            sd.first[c] = __builtin_amdgcn_readfirstlane(misc[M_FIRST + c]);
+        for (int q = 0; q < 4; ++q) {
+            selA[q] = __builtin_amdgcn_readfirstlane(misc[M_SELA + q]);
+            selB[q] = __builtin_amdgcn_readfirstlane(misc[M_SELB + q]);
+        }
+        const uint32_t edA = __builtin_amdgcn_readfirstlane(misc[M_EDA]);
+        const uint32_t edB = __builtin_amdgcn_readfirstlane(misc[M_EDB]);
+        PSY_PROF_MARK(2);
+
+        auto tmat = [&](const uint4 &d, uint32_t (&T)[4]) __attribute__((always_inline)) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) T[q] = perm(d.y, d.x, selA[q]) | perm(d.w, d.z, selB[q]);
+        };
+        auto edges = [&](const uint4 &d) __attribute__((always_inline)) -> uint32_t {
+            return perm(d.y, d.x, edA) | perm(d.w, d.z, edB);
+        };
+        // valid slots of a group holding vb message bytes
+        auto vmask = [&](uint32_t vb) __attribute__((always_inline)) -> uint32_t {
+            const uint32_t nvw = vb / WS;
+            if (nvw >= (uint32_t)WPG) return 0xffffu;
+            uint32_t v = (1u << (nvw * k0)) - 1u;
+            if (ns2) v |= ((1u << (nvw * k1)) - 1u) << L0;
+            return v;
+        };
+        // run-start mask of the 16 slots (bit j: slot j differs from the stream byte before)
+        auto run_mask = [&](const uint32_t (&T)[4], uint32_t ed, uint32_t edc, uint32_t g,
+                            uint32_t V) __attribute__((always_inline)) -> uint32_t {
+            const uint32_t pe = wave_shr1(ed, edc);  // previous group's edges
+            const uint32_t P0 = perm(T[3], pe, 0x06050400u);
+            const uint32_t X[4] = {T[0] ^ P0, T[1] ^ T[0], T[2] ^ T[1], T[3] ^ T[2]};
+            uint32_t m = 0;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                sd.selA[c][q] = __builtin_amdgcn_readfirstlane(misc[M_SELA + 4 * c + q]);
-                sd.selB[c][q] = __builtin_amdgcn_readfirstlane(misc[M_SELB + 4 * c + q]);
+                const uint32_t y = ((X[q] & 0x7f7f7f7fu) + 0x7f7f7f7fu) | X[q];
+                m |= (y >> (7 - q)) & (0x01010101u << q);
             }
-        }
-        if (sd.ns < 2) sd.k[1] = 0;  // stream 1 absent: every group has L = 0 for it
-        // the byte of the previous group that precedes stream c's first byte of a group
-        uint32_t pq[2], pb[2];
-#pragma unroll
-        for (int c = 0; c < 2; ++c) {
-            const uint32_t i = 16 - WS + sd.last[c];
-            pq[c] = i >> 2;
-            pb[c] = 8 * (i & 3);
-        }
-
-        auto gather = [&](const uint4 &d, int c, uint32_t (&s)[4]) __attribute__((always_inline)) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                s[q] = __builtin_amdgcn_perm(d.y, d.x, sd.selA[c][q]) | __builtin_amdgcn_perm(d.w, d.z, sd.selB[c][q]);
+            m = (m | (m >> 4)) & 0x00ff00ffu;
+            m = (m | (m >> 8)) & 0xffffu;
+            if (ns2) {
+                const uint32_t fx = ((ed >> 16) ^ (pe >> 8)) & 0xffu;
+                m = (m & ~(1u << L0)) | ((fx ? 1u : 0u) << L0);
+            }
+            if (g == 0) m |= 1u | (ns2 ? (1u << L0) : 0u);
+            return m & V;
         };
-        // run-start masks of both streams for round r (stream 1 in bits 16..31)
-        auto run_masks = [&](uint32_t r, const uint4 &d) __attribute__((always_inline)) -> uint32_t {
-            const uint32_t g = gw0 + r * 64 + lane;
-            const uint32_t nvw = vbytes(g) / WS;
+        // packed (stream 1 in the high half) round-relative last start + 1 of a start mask
+        auto last_starts = [&](uint32_t m) __attribute__((always_inline)) -> uint32_t {
+            const uint32_t m0 = m & lowL0;
+            uint32_t lr = m0 ? (uint32_t)lane * Ls[0] + hibit(m0) + 1u : 0u;
+            if (ns2) {
+                const uint32_t m1 = m >> L0;
+                lr |= (m1 ? (uint32_t)lane * Ls[1] + hibit(m1) + 1u : 0u) << 16;
+            }
+            return lr;
+        };
+        // the 255-cap bit of the run carried into each group (simple_rle_compress :568).
+        // exc: packed exclusive scan of last run start + 1 (round-relative); rcarry:
+        // absolute last run start + 1 before the round (0 = none); rb: round base positions.
+        auto cap_bits = [&](uint32_t m, uint32_t exc, const uint32_t (&rcarry)[2], const uint32_t (&rb)[2],
+                            uint32_t g, uint32_t V) __attribute__((always_inline)) -> uint32_t {
+            uint32_t need = 0;
+            uint32_t csp[2] = {0, 0}, Lv[2] = {0, 0};
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                if (c == 1 && !ns2) break;
+                const uint32_t er = (exc >> (16 * c)) & 0xffffu;
+                csp[c] = er ? rb[c] + er : rcarry[c];
+                Lv[c] = c == 0 ? popc(V & lowL0) : popc(V >> L0);
+                need |= (csp[c] && g * Ls[c] + Lv[c] >= csp[c] + 255u) ? 1u : 0u;
+            }
+            if (!__any(need)) return 0u;  // no run of >= 255 bytes reaches this round
             uint32_t out = 0;
 #pragma unroll
             for (int c = 0; c < 2; ++c) {
-                if (sd.k[c] == 0) continue;  // uniform
-                const uint32_t L = nvw * sd.k[c];
-                // previous group's last word from lane-1; lane 0 reads it from memory
-                const uint32_t pw = shfl_up1(dword_of(d, pq[c]));
-                uint32_t prevb = (pw >> pb[c]) & 0xffu;
-                if (lane == 0 && g > 0 && L) prevb = base[16ull * g - WS + sd.last[c]];
-                uint32_t s[4];
-                gather(d, c, s);
-                uint32_t m = neq_prev_mask4(s[0], prevb << 24) | (neq_prev_mask4(s[1], s[0]) << 4) |
-                             (neq_prev_mask4(s[2], s[1]) << 8) | (neq_prev_mask4(s[3], s[2]) << 12);
-                if (g == 0) m |= 1u;
-                m = L ? (m & ((1u << L) - 1u)) : 0u;
-                out |= m << (16 * c);
+                if (c == 1 && !ns2) break;
+                const uint32_t mc = c == 0 ? (m & lowL0) : (m >> L0);
+                if (csp[c] && !(mc & 1u) && Lv[c]) {
+                    const uint32_t d = g * Ls[c] + 1u - csp[c];  // >= 1
+                    const uint32_t rel = 255u * ((d + 254u) / 255u) - d;
+                    const uint32_t fs = lobit(mc | (1u << Lv[c]));
+                    if (rel < fs) out |= 1u << (rel + (c ? L0 : 0u));
+                }
             }
             return out;
         };
-        // chunk-start masks for round r given run-start masks m and the carried maximum of
-        // (last run start + 1) before the round; advances the carry (rm).
-        auto chunk_masks = [&](uint32_t r, uint32_t m, uint32_t (&rm)[2]) __attribute__((always_inline)) -> uint32_t {
-            const uint32_t g = gw0 + r * 64 + lane;
-            const uint32_t nvw = vbytes(g) / WS;
-            uint32_t chunkp = 0;
-#pragma unroll
-            for (int c = 0; c < 2; ++c) {
-                if (sd.k[c] == 0) continue;
-                const uint32_t mc = (m >> (16 * c)) & 0xffffu;
-                const uint32_t L = nvw * sd.k[c];
-                const uint32_t gpos = g * WPG * sd.k[c];
-                const uint32_t mv = mc ? gpos + hibit(mc) + 1u : 0u;
-                const uint32_t inc = wave_incl_scan<OpMax>(mv);
-                uint32_t cs_enc = wave_shift_up1(inc);
-                cs_enc = umax(cs_enc, rm[c]);
-                rm[c] = umax(rm[c], rdlane(inc, 63));
-                // 255-cap inside the carried run (simple_rle_compress :568)
-                uint32_t cap = 0;
-                if (L && !(mc & 1u) && cs_enc) {
-                    const uint32_t cs = cs_enc - 1;
-                    const uint32_t fs = mc ? lobit(mc) : L;
-                    const uint32_t cpos = cs + 255u * ((gpos - cs + 254u) / 255u);
-                    if (cpos < gpos + fs) cap = 1u << (cpos - gpos);
-                }
-                chunkp |= (mc | cap) << (16 * c);
-            }
-            return chunkp;
+        // chunk-start mask of round r given its run-start mask; advances the run carry
+        auto chunk_round = [&](uint32_t r, uint32_t m, uint32_t (&rcarry)[2], uint32_t g,
+                               uint32_t V) __attribute__((always_inline)) -> uint32_t {
+            const uint32_t rb[2] = {(gw0 + r * 64) * Ls[0], (gw0 + r * 64) * Ls[1]};
+            const uint32_t inc = wave_incl_scan<OpPkMax>(last_starts(m));
+            const uint32_t exc = wave_shr1(inc, 0u);
+            const uint32_t C = m | cap_bits(m, exc, rcarry, rb, g, V);
+            const uint32_t i63 = rdlane(inc, 63);
+            if (i63 & 0xffffu) rcarry[0] = umax(rcarry[0], rb[0] + (i63 & 0xffffu));
+            if (i63 >> 16) rcarry[1] = umax(rcarry[1], rb[1] + (i63 >> 16));
+            return C;
         };
+
+        // edges of the group before this wave's first group (carry into round 0)
+        uint32_t edc0 = 0;
+        if (gw0 > 0 && gw0 - 1 < ngroups) edc0 = __builtin_amdgcn_readfirstlane(edges(load_group(gw0 - 1)));
 
         // ---------------------------------------------------------- pass A1: run starts
         uint32_t wmax[2] = {0, 0};
-        for_rounds([&](uint32_t r, const uint4 d, uint32_t &cm) __attribute__((always_inline)) {
-            const uint32_t g = gw0 + r * 64 + lane;
-            const uint32_t m = run_masks(r, d);
-            cm = m;  // kept for A2 (resident messages)
-#pragma unroll
-            for (int c = 0; c < 2; ++c) {
-                if (sd.k[c] == 0) continue;
-                const uint32_t mc = (m >> (16 * c)) & 0xffffu;
-                const uint32_t gpos = g * WPG * sd.k[c];
-                const uint32_t mv = mc ? gpos + hibit(mc) + 1u : 0u;
-                wmax[c] = umax(wmax[c], wave_reduce<OpMax>(mv));
-            }
-        });
+        {
+            uint32_t edc = edc0;
+            for_rounds([&](uint32_t r, const uint4 d, uint32_t &cm) __attribute__((always_inline)) {
+                const uint32_t g = gw0 + r * 64 + lane;
+                uint32_t T[4];
+                tmat(d, T);
+                const uint32_t ed = edges(d);
+                const uint32_t V = full_round(r) ? 0xffffu : vmask(vbytes(g));
+                const uint32_t m = run_mask(T, ed, edc, g, V);
+                edc = rdlane(ed, 63);
+                cm = m;
+                const uint32_t m0 = m & lowL0;
+                if (m0) wmax[0] = umax(wmax[0], g * Ls[0] + hibit(m0) + 1u);
+                if (ns2) {
+                    const uint32_t m1 = m >> L0;
+                    if (m1) wmax[1] = umax(wmax[1], g * Ls[1] + hibit(m1) + 1u);
+                }
+            });
+        }
+        wmax[0] = wave_reduce<OpMax>(wmax[0]);
+        wmax[1] = wave_reduce<OpMax>(wmax[1]);
         if (lane == 0) {
             slots[wv * 8 + 0] = wmax[0];
             slots[wv * 8 + 1] = wmax[1];
@@ -479,52 +566,59 @@ __global__ __launch_bounds__(TEAM) void tdt_encode_kernel(EncodeArgs a) {
             }
         rin[0] = __builtin_amdgcn_readfirstlane(rin[0]);
         rin[1] = __builtin_amdgcn_readfirstlane(rin[1]);
+        PSY_PROF_MARK(3);
 
         // ---------------------------------------------------------- pass A2: chunk starts
-        uint32_t rm[2] = {rin[0], rin[1]};
-        uint32_t psum[2] = {0, 0}, cmaxw[2] = {0, 0};
-        uint32_t fb0 = 0;  // chunk bit 0 of this wave's first group (stream 1 in bit 16)
-        for_rounds([&](uint32_t r, const uint4 d, uint32_t &cm) __attribute__((always_inline)) {
-            const uint32_t g = gw0 + r * 64 + lane;
-            const uint32_t m = resident ? cm : run_masks(r, d);
-            const uint32_t chunkp = chunk_masks(r, m, rm);
-            if (resident) cm = chunkp;  // kept for pass B
-#pragma unroll
-            for (int c = 0; c < 2; ++c) {
-                if (sd.k[c] == 0) continue;
-                const uint32_t ch = (chunkp >> (16 * c)) & 0xffffu;
-                const uint32_t gpos = g * WPG * sd.k[c];
-                psum[c] += wave_reduce<OpAdd>(popc(ch));
-                cmaxw[c] = umax(cmaxw[c], wave_reduce<OpMax>(ch ? gpos + hibit(ch) + 1u : 0u));
-            }
-            if (r == 0) fb0 = rdlane(chunkp, 0) & 0x10001u;
-        });
+        uint32_t pc0 = 0, pc1 = 0;  // per-lane chunk-start counts
+        uint32_t fb = 0;            // chunk bits of this wave's first group
+        {
+            uint32_t rcarry[2] = {rin[0], rin[1]};
+            uint32_t edc = edc0;
+            for_rounds([&](uint32_t r, const uint4 d, uint32_t &cm) __attribute__((always_inline)) {
+                const uint32_t g = gw0 + r * 64 + lane;
+                const uint32_t V = full_round(r) ? 0xffffu : vmask(vbytes(g));
+                uint32_t m;
+                if (resident) {
+                    m = cm;
+                } else {
+                    uint32_t T[4];
+                    tmat(d, T);
+                    const uint32_t ed = edges(d);
+                    m = run_mask(T, ed, edc, g, V);
+                    edc = rdlane(ed, 63);
+                }
+                const uint32_t C = chunk_round(r, m, rcarry, g, V);
+                cm = C;
+                pc0 += popc(C & lowL0);
+                pc1 += popc(C >> L0);
+                if (r == 0) fb = rdlane(C, 0);
+            });
+        }
+        pc0 = wave_reduce<OpAdd>(pc0);
+        pc1 = ns2 ? wave_reduce<OpAdd>(pc1) : 0u;
         if (lane == 0) {
-            slots[wv * 8 + 2] = psum[0];
-            slots[wv * 8 + 3] = psum[1];
-            slots[wv * 8 + 4] = fb0;
-            slots[wv * 8 + 5] = cmaxw[0];
-            slots[wv * 8 + 6] = cmaxw[1];
+            slots[wv * 8 + 2] = pc0;
+            slots[wv * 8 + 3] = pc1;
+            slots[wv * 8 + 4] = fb;
         }
         team_sync<W>();
-        uint32_t pin[2] = {0, 0}, ptot[2] = {0, 0}, cin[2] = {0, 0};
+        PSY_PROF_MARK(4);
+        uint32_t pin[2] = {0, 0}, ptot[2] = {0, 0};
 #pragma unroll
         for (int ww = 0; ww < W; ++ww) {
             const uint32_t s0 = slots[ww * 8 + 2], s1 = slots[ww * 8 + 3];
             if (ww < wv) {
                 pin[0] += s0;
                 pin[1] += s1;
-                cin[0] = umax(cin[0], slots[ww * 8 + 5]);
-                cin[1] = umax(cin[1], slots[ww * 8 + 6]);
             }
             ptot[0] += s0;
             ptot[1] += s1;
         }
         const uint32_t nfb = __builtin_amdgcn_readfirstlane((wv + 1 < W) ? slots[(wv + 1) * 8 + 4] : 0u);
         const uint32_t P0 = __builtin_amdgcn_readfirstlane(ptot[0]);
-        const uint32_t P1 = sd.ns > 1 ? __builtin_amdgcn_readfirstlane(ptot[1]) : 0u;
+        const uint32_t P1 = ns2 ? __builtin_amdgcn_readfirstlane(ptot[1]) : 0u;
         const uint32_t hdr = 20 + 4 * WS;
-        const uint64_t E = hdr + (4 + 2ull * P0) + (sd.ns > 1 ? 4 + 2ull * P1 : 0);
+        const uint64_t E = hdr + (4 + 2ull * P0) + (ns2 ? 4 + 2ull * P1 : 0);
         if (tid == 0) {
             uint64_t b = lookback_excl(a.lookback, msg, E, a.errflags);
             *reinterpret_cast<uint64_t *>(misc + M_BASE) = b;
@@ -546,121 +640,205 @@ __global__ __launch_bounds__(TEAM) void tdt_encode_kernel(EncodeArgs a) {
             uint32_t v;
             if (f == 0) v = kMagicTDT;
             else if (f == 1) v = n32;
-            else if (f == 2) v = sd.ns;
+            else if (f == 2) v = ns;
             else if (f == 3 || f == 4) v = WS;
             else v = misc[M_MAP + (f - 5)];
             dst[t] = (uint8_t)(v >> sh);
         }
         if (tid < 8) {
             const int c = tid >> 2, sh = 8 * (tid & 3);
-            if ((uint32_t)c < sd.ns) {
+            if ((uint32_t)c < ns) {
                 const uint32_t len = 2 * (c ? P1 : P0);
                 dst[sdata[c] - 4 + (tid & 3)] = (uint8_t)(len >> sh);
             }
         }
+        PSY_PROF_MARK(5);
 
         // ---------------------------------------------------------- pass B: emit pairs
-        // Everything below is wave-local: per-wave LDS staging, no workgroup barrier.
+        // Wave-local from here on: per-wave LDS staging, no workgroup barrier.
         const uint32_t wst = Lay::OFF_UNION + wv * Lay::WSTAGE;
         uint32_t pr[2] = {(uint32_t)__builtin_amdgcn_readfirstlane(pin[0]), (uint32_t)__builtin_amdgcn_readfirstlane(pin[1])};
-        uint32_t cmc[2] = {(uint32_t)__builtin_amdgcn_readfirstlane(cin[0]), (uint32_t)__builtin_amdgcn_readfirstlane(cin[1])};
-        uint32_t rmB[2] = {rin[0], rin[1]};
-        for_rounds([&](uint32_t r, const uint4 d, uint32_t &cm) __attribute__((always_inline)) {
+        // last chunk start + 1 before this wave: inside the run carried in (start rin - 1),
+        // chunks start every 255 bytes (simple_rle_compress :568)
+        uint32_t ccarry[2] = {0, 0};
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            const uint32_t W0 = gw0 * Ls[c];
+            if (rin[c] && W0 > 0) {
+                const uint32_t rs = rin[c] - 1;
+                ccarry[c] = rs + 255u * ((W0 - 1 - rs) / 255u) + 1u;
+            }
+        }
+
+        // Emit the pairs of round r: d its data, C its chunk-start mask, nxt63 the chunk bits
+        // of the group after lane 63's (combined layout).
+        auto emit = [&](uint32_t r, const uint4 &d, uint32_t C, uint32_t nxt63) __attribute__((always_inline)) {
             const uint32_t g = gw0 + r * 64 + lane;
-            const uint32_t nvw = vbytes(g) / WS;
-            const bool last_group = 16ull * (g + 1) >= n;
-            const uint32_t chunkp = resident ? cm : chunk_masks(r, run_masks(r, d), rmB);
-            const uint32_t nxt = shfl_down1(chunkp);  // next group's chunk starts (lanes < 63)
+            // the message does not end inside (or before the end of) this round
+            const bool inner = 16ull * (gw0 + r * 64 + 64) < n;
+            const uint32_t V = inner ? 0xffffu : vmask(vbytes(g));
+            uint32_t T[4];
+            tmat(d, T);
+            const uint32_t ed = edges(d);
+            const uint32_t rb[2] = {(gw0 + r * 64) * Ls[0], (gw0 + r * 64) * Ls[1]};
+            // last chunk start + 1 before each group (packed, round-relative; 0 = earlier)
+            const uint32_t cinc = wave_incl_scan<OpPkMax>(last_starts(C));
+            const uint32_t cexc = wave_shr1(cinc, 0u);
+            // chunk END mask: slot j ends a chunk when the stream's next slot starts one
+            const uint32_t nb = wave_shl1(C, nxt63);
+            uint32_t e = (C >> 1) & 0x7fffu;
+            if (L0 > 0) e = (e & ~(1u << (L0 - 1))) | ((nb & 1u) << (L0 - 1));
+            if (ns2) e |= ((nb >> L0) & 1u) << 15;
+            if (!inner) {
+                if (g == ngroups - 1) {  // the message's last group closes every chunk
+                    const uint32_t lv0 = popc(V & lowL0), lv1 = popc(V >> L0);
+                    e = (C >> 1) & V;
+                    if (lv0) e |= 1u << (lv0 - 1);
+                    if (ns2 && lv1) e |= 1u << (L0 + lv1 - 1);
+                }
+                e &= V;
+            }
+            // pair indices: packed sum-scan of chunk starts
+            const uint32_t pc = popc(C & lowL0) | (popc(C >> L0) << 16);
+            const uint32_t pinc = wave_incl_scan<OpAdd>(pc);
+            const uint32_t pexc = pinc - pc;
+            const uint32_t ptr = rdlane(pinc, 63);
+            const uint32_t C_l0 = rdlane(C, 0), V_l0 = rdlane(V, 0);
+            uint32_t k0c[2], ends[2], rbs[2], base[2];
+            uint64_t gdst[2];
 #pragma unroll
             for (int c = 0; c < 2; ++c) {
-                if (sd.k[c] == 0) continue;  // uniform
-                const uint32_t L = nvw * sd.k[c];
-                const uint32_t gpos = g * WPG * sd.k[c];
-                const uint32_t ch = (chunkp >> (16 * c)) & 0xffffu;
-                // last chunk start (+1) before this group: wave max-scan + carry
-                const uint32_t lc = ch ? gpos + hibit(ch) + 1u : 0u;
-                const uint32_t cinc = wave_incl_scan<OpMax>(lc);
-                uint32_t ccs = wave_shift_up1(cinc);
-                ccs = umax(ccs, cmc[c]);
-                const uint32_t ctot = rdlane(cinc, 63);
-                // chunk starts before this group → pair indices
-                const uint32_t pc = popc(ch);
-                const uint32_t pinc = wave_incl_scan<OpAdd>(pc);
-                const uint32_t pbase = pr[c] + pinc - pc;
-                const uint32_t rtot = rdlane(pinc, 63);
-                uint32_t s[4];
-                gather(d, c, s);
-                // chunk END at slot L-1 iff the next stream byte starts a chunk
-                uint32_t e = 0;
-                if (L) {
-                    bool lend;
-                    if (last_group) {
-                        lend = true;
-                    } else if (lane < 63) {
-                        lend = (nxt >> (16 * c)) & 1u;
-                    } else if (r + 1 < RW) {
-                        // next group = lane 0 of this wave's next round: new run, or exactly
-                        // 255 bytes after the start of the chunk holding the last byte
-                        const uint32_t nb = base[16ull * (g + 1) + sd.first[c]];
-                        const uint32_t lb = (s[(L - 1) >> 2] >> (8 * ((L - 1) & 3))) & 0xffu;
-                        const uint32_t lcs = ch ? gpos + hibit(ch) : ccs - 1u;
-                        lend = (nb != lb) || (gpos + L - lcs == 255u);
-                    } else {
-                        lend = (nfb >> (16 * c)) & 1u;  // next wave's first group
-                    }
-                    e = ((ch >> 1) | ((uint32_t)lend << (L - 1))) & ((1u << L) - 1u);
-                }
-                // staging window of this wave-round: the pairs ending here, [k0, k0 + ends)
-                const uint32_t f0 = rdlane(ch, 0);
-                const uint32_t dang = (rdlane(L, 0) && !(f0 & 1u)) ? 1u : 0u;
-                const uint32_t k0 = pr[c] - dang;
-                const uint32_t ends = wave_reduce<OpAdd>(popc(e));
-                const uint64_t gdst = (uint64_t)(uintptr_t)dst + sdata[c] + 2ull * k0;
-                const uint32_t ra = (uint32_t)(gdst & 15);
-                const uint32_t rb = wst + c * Lay::WREGION + ra;
-                // start of the chunk holding slot 0, relative to gpos (<= 0)
-                int cst = (!(ch & 1u) && ccs) ? (int)(ccs - 1u) - (int)gpos : 0;
-                uint32_t nst = 0;  // chunk starts at slots <= j
+                const uint32_t off = c ? L0 : 0u;
+                const uint32_t dang = (((V_l0 >> off) & 1u) && !((C_l0 >> off) & 1u)) ? 1u : 0u;
+                const uint32_t dout = inner ? (((nxt63 >> off) & 1u) ? 0u : 1u) : 0u;
+                const uint32_t tot = (ptr >> (16 * c)) & 0xffffu;
+                k0c[c] = pr[c] - dang;
+                ends[c] = (Ls[c] == 0) ? 0u : tot + dang - dout;
+                gdst[c] = (uint64_t)(uintptr_t)dst + sdata[c] + 2ull * k0c[c];
+                rbs[c] = wst + c * Lay::WREGION + 16u + (uint32_t)(gdst[c] & 15);
+                const uint32_t fi = pr[c] + ((pexc >> (16 * c)) & 0xffffu) - (((C >> off) & 1u) ? 0u : 1u);
+                base[c] = rbs[c] + 2u * (fi - k0c[c]);
+            }
+            const uint32_t E2 = spread2(e);
+            const uint32_t base1p = base[1] - 2u * popc(e & lowL0);
+            // sweep 1: every valid slot, ascending
+            auto sweep = [&](auto odd) __attribute__((always_inline)) {
 #pragma unroll
-                for (int j = 0; j < 16; ++j) {
-                    const uint32_t isst = (ch >> j) & 1u;
-                    nst += isst;
-                    cst = isst ? j : cst;
-                    if ((e >> j) & 1u) {
-                        const uint32_t rel = pbase + nst - 1u - k0;
-                        const uint32_t cnt = (uint32_t)(j - cst + 1);
-                        const uint32_t val = (s[j >> 2] >> (8 * (j & 3))) & 0xffu;
-                        if (rel < ends) {
-                            smem[rb + 2 * rel] = (uint8_t)cnt;
-                            smem[rb + 2 * rel + 1] = (uint8_t)val;
-                        } else {
-                            atomicOr(a.errflags, 2u);
+                for (int j = 0; j < 16; j += 2) {
+                    const int q = j & 3, t = j >> 2;
+                    const uint32_t ca = ffbh_u32(C << (31 - j)), cb = ffbh_u32(C << (30 - j));
+                    const uint32_t pair = (perm(cb, ca, 0x0c040c00u) + 0x00010001u) |
+                                          perm(T[q + 1], T[q], 0x0cu | ((uint32_t)t << 8) | (0x0cu << 16) |
+                                                                   ((uint32_t)(4 + t) << 24));
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const int jj = j + h;
+                        const uint32_t ad = ((uint32_t)jj < L0 ? base[0] : base1p) +
+                                            (jj ? popc(E2 & ((1u << (2 * jj)) - 1u)) : 0u);
+                        const uint32_t pv = h ? (pair >> 16) : (pair & 0xffffu);
+                        if (inner || ((V >> jj) & 1u)) {
+                            if constexpr (decltype(odd)::value) {
+                                smem[ad] = (uint8_t)pv;
+                                smem[ad + 1] = (uint8_t)(pv >> 8);
+                            } else {
+                                *reinterpret_cast<uint16_t *>(smem + ad) = (uint16_t)pv;
+                            }
                         }
                     }
                 }
-                team_sync<1>();  // this wave's staging writes are visible to its other lanes
-                uint32_t len = 2u * ends;
-                if (len && sdata[c] + 2ull * k0 + len > E) {  // never for a consistent round
+                // sweep 2: the first pair ending in this group, per stream (its chunk may have
+                // begun in an earlier group; also repairs same-instruction collisions)
+#pragma unroll
+                for (int c = 0; c < 2; ++c) {
+                    if (Ls[c] == 0) continue;
+                    const uint32_t off = c ? L0 : 0u;
+                    const uint32_t ec = c ? (e >> L0) : (e & lowL0);
+                    if (ec) {
+                        const uint32_t jf = lobit(ec);
+                        uint32_t cnt;
+                        if ((C >> off) & 1u) {
+                            cnt = jf + 1u;
+                        } else {
+                            const uint32_t cer = (cexc >> (16 * c)) & 0xffffu;
+                            const uint32_t lcp = cer ? rb[c] + cer : ccarry[c];  // last chunk start + 1
+                            cnt = g * Ls[c] + jf + 2u - lcp;
+                        }
+                        const uint32_t val = c ? ((ed >> 16) & 0xffu) : (T[0] & 0xffu);
+                        const uint32_t pv = (cnt & 0xffu) | (val << 8);
+                        if constexpr (decltype(odd)::value) {
+                            smem[base[c]] = (uint8_t)pv;
+                            smem[base[c] + 1] = (uint8_t)(pv >> 8);
+                        } else {
+                            *reinterpret_cast<uint16_t *>(smem + base[c]) = (uint16_t)pv;
+                        }
+                    }
+                }
+            };
+            if (((gdst[0] | gdst[1]) & 1) == 0) sweep(std::false_type{});
+            else sweep(std::true_type{});
+            team_sync<1>();  // this wave's staging writes are visible to its other lanes
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                if (Ls[c] == 0) continue;
+                uint32_t len = 2u * ends[c];
+                if (len && sdata[c] + 2ull * k0c[c] + len > E) {  // never for a consistent round
                     if (lane == 0) atomicOr(a.errflags, 4u);
                     len = 0;
                 }
                 if (len) {
-                    uint8_t *gd = dst + sdata[c] + 2ull * k0;
+                    uint8_t *gd = dst + sdata[c] + 2ull * k0c[c];
+                    const uint32_t ra = (uint32_t)(gdst[c] & 15);
                     const uint32_t head0 = (16u - ra) & 15u;
                     const uint32_t head = head0 < len ? head0 : len;
                     const uint32_t body = (len - head) & ~15u;
-                    if ((uint32_t)lane < head) gd[lane] = smem[rb + lane];
+                    if ((uint32_t)lane < head) gd[lane] = smem[rbs[c] + lane];
                     for (uint32_t k = lane; k < body / 16; k += 64)
                         *reinterpret_cast<uint4 *>(gd + head + 16 * k) =
-                            *reinterpret_cast<const uint4 *>(smem + rb + head + 16 * k);
+                            *reinterpret_cast<const uint4 *>(smem + rbs[c] + head + 16 * k);
                     const uint32_t tail = len - head - body;
-                    if ((uint32_t)lane < tail) gd[head + body + lane] = smem[rb + head + body + lane];
+                    if ((uint32_t)lane < tail) gd[head + body + lane] = smem[rbs[c] + head + body + lane];
                 }
-                team_sync<1>();
-                pr[c] += rtot;
-                cmc[c] = umax(cmc[c], ctot);
+                pr[c] += (ptr >> (16 * c)) & 0xffffu;
+                const uint32_t ci = (rdlane(cinc, 63) >> (16 * c)) & 0xffffu;
+                if (ci) ccarry[c] = umax(ccarry[c], rb[c] + ci);
             }
-        });
+            team_sync<1>();  // the window is rewritten by the next round
+        };
+
+        if (resident) {
+            for (uint32_t r = 0; r < (uint32_t)G; ++r) {
+                if (r < RW) emit(r, dres[0], cres[0], r + 1 < RW ? rdlane(cres[1], 0) : nfb);
+                rotate();
+            }
+        } else {
+            // chunk masks are computed one round ahead (lane 63 needs the next round's)
+            uint32_t rcarry[2] = {rin[0], rin[1]};
+            uint32_t edc = edc0;
+            auto chunk_of = [&](uint32_t r, const uint4 &d) __attribute__((always_inline)) -> uint32_t {
+                const uint32_t g = gw0 + r * 64 + lane;
+                const uint32_t V = full_round(r) ? 0xffffu : vmask(vbytes(g));
+                uint32_t T[4];
+                tmat(d, T);
+                const uint32_t ed = edges(d);
+                const uint32_t m = run_mask(T, ed, edc, g, V);
+                edc = rdlane(ed, 63);
+                return chunk_round(r, m, rcarry, g, V);
+            };
+            uint4 dc = load_group(gw0 + lane);
+            uint32_t Cc = chunk_of(0, dc);
+            for (uint32_t r = 0; r < RW; ++r) {
+                uint4 dn = make_uint4(0, 0, 0, 0);
+                uint32_t Cn = 0;
+                if (r + 1 < RW) {
+                    dn = load_group(gw0 + (r + 1) * 64 + lane);
+                    Cn = chunk_of(r + 1, dn);
+                }
+                emit(r, dc, Cc, r + 1 < RW ? rdlane(Cn, 0) : nfb);
+                dc = dn;
+                Cc = Cn;
+            }
+        }
+        PSY_PROF_MARK(6);
     }
 }
 

@@ -64,10 +64,10 @@ def _ptr(t) -> int:
 class TdtCodec:
     """Batched TDT codec bound to one HIP device."""
 
-    def __init__(self, config: TDTConfig | None = None, device: int = 0):
+    def __init__(self, config: TDTConfig | None = None, device: int = 0, lib=None):
         self.config = config or TDTConfig()
         self.device = device
-        self._lib = _lib.load()
+        self._lib = lib if lib is not None else _lib.load()  # `lib`: diagnostic builds only
         h = C.c_void_p()
         cfg = self.config.to_c()
         check(self._lib.tdt_ctx_create(device, C.byref(cfg), C.byref(h)))

@@ -16,6 +16,8 @@ using namespace psy;
 //   [1155,1219) perm(in[l], in[l+64], sel[l%8])
 //   [1219,1283) alignbyte(in[l], in[l+64], 3)
 //   [1283,1347) wave_shift_up1(in[l])
+//   [1347,1411) wave_shr1(in[l], 77)   [1411,1475) wave_shl1(in[l], 99)
+//   [1475,1539) packed u16 max-scan     [1539,1603) ffbh_u32(in[l] >> (l % 33))
 __global__ __launch_bounds__(256) void selftest_kernel(const uint32_t *in, uint32_t *out) {
     __shared__ uint32_t slots[2 * 4 * 4];
     const int t = threadIdx.x, lane = t & 63;
@@ -42,6 +44,11 @@ __global__ __launch_bounds__(256) void selftest_kernel(const uint32_t *in, uint3
         out[1155 + t] = __builtin_amdgcn_perm(x, y, sels[lane & 7]);
         out[1219 + t] = __builtin_amdgcn_alignbyte(x, y, 3);
         out[1283 + t] = wave_shift_up1(x);
+        out[1347 + t] = wave_shr1(x, 77u);
+        out[1411 + t] = wave_shl1(x, 99u);
+        out[1475 + t] = wave_incl_scan<OpPkMax>(x * 2654435761u);
+        const uint32_t sh = (uint32_t)(t % 33);
+        out[1539 + t] = ffbh_u32(sh == 32 ? 0u : (x >> sh));
     }
 }
 

@@ -36,7 +36,7 @@ def test_primitives():
     x[64:128] = rng.integers(0, 4, 64) * 0x01010101  # byte-equal patterns for the mask test
     x[5] = x[69] = 0x11223344
     d_in = torch.from_numpy(x.view(np.int32).copy()).cuda()
-    d_out = torch.zeros(1400, dtype=torch.int32, device="cuda")
+    d_out = torch.zeros(1700, dtype=torch.int32, device="cuda")
     assert lib.selftest_run(C.c_void_p(d_in.data_ptr()), C.c_void_p(d_out.data_ptr())) == 0
     o = d_out.cpu().numpy().view(np.uint32)
     xs = x.astype(np.uint64)
@@ -58,3 +58,15 @@ def test_primitives():
         assert o[1155 + l] == host_perm(int(x[l]), int(x[l + 64]), sels[l & 7]), ("perm", l)
         assert o[1219 + l] == (((int(x[l]) << 32 | int(x[l + 64])) >> 24) & 0xFFFFFFFF), ("alignbyte", l)
         assert o[1283 + l] == (x[l - 1] if l else 0), ("shift_up", l)
+    for l in range(64):
+        assert o[1347 + l] == (x[l - 1] if l else 77), ("wave_shr1", l)
+        assert o[1411 + l] == (x[l + 1] if l < 63 else 99), ("wave_shl1", l)
+    h = (x[:64].astype(np.uint64) * 2654435761) & 0xFFFFFFFF
+    lo = np.maximum.accumulate(h & 0xFFFF)
+    hi = np.maximum.accumulate(h >> 16)
+    assert np.array_equal(o[1475:1539], (lo | (hi << 16)).astype(np.uint32)), "packed u16 max-scan"
+    for l in range(64):
+        sh = l % 33
+        v = 0 if sh == 32 else int(x[l]) >> sh
+        want = 0xFFFFFFFF if v == 0 else 32 - v.bit_length()
+        assert o[1539 + l] == want, ("ffbh", l, v)
