@@ -4,9 +4,10 @@
 Workload (BASELINE.json configs[2] = SURVEY.md §8(d) C3): per GPU, 262,144 messages of
 64 KiB float32 "gradient-like" payload (70 % exact 0.0f, else N(0, 0.01) — the
 GRADIENTS generator of the reference's tdt_compression_benchmark.cpp:52-66), generated on
-the device with a fixed seed.  One STEP = tdt_encode_batch over the whole batch (compacted
-blobs + offsets) followed by tdt_decode_batch of those blobs (compacted payloads), inputs
-already resident in HBM.  Compression is on (bandwidth 10 Mbps < 100 Mbps threshold) and the
+the device with a fixed seed.  One STEP = tdt_encode_slots + tdt_encode_batch_into over the
+whole batch (each blob in its own slot, lengths returned — one vector per message, as the
+reference's encode returns) followed by tdt_decode_slots + tdt_decode_batch_into of those
+blobs, inputs already resident in HBM.  Compression is on (bandwidth 10 Mbps < 100 Mbps threshold) and the
 mapping is computed from every word (the reference's sample_fraction = 1.0, deterministic).
 
 value = payload bytes round-tripped by all ranks / max-over-ranks wall time, in GiB/s.
@@ -130,22 +131,33 @@ def main():
     codec = TdtCodec(TDTConfig(sample_fraction=1.0), device=local)
     codec.set_metrics(10.0, 1.0, 0.5)  # slow network → compression on (tdt_compression.hpp:200)
     codec.set_size_hint(mb)
+    # Slotted batches (tdt_encode_batch_into / tdt_decode_batch_into): blob i lands in its own
+    # slot of the output buffer, as the reference returns one vector per message; the slot
+    # offsets (prefix sums of the encode bounds / of the decoded sizes) are computed on the
+    # device inside every step.
     cap = n * codec.encode_bound(mb)
     enc = torch.empty(cap, dtype=torch.uint8, device=dev)
-    eoff = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    eslot = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    elen = torch.empty(n, dtype=torch.int64, device=dev)
     est = torch.empty(n, dtype=torch.int32, device=dev)
     dec = torch.empty(n * mb, dtype=torch.uint8, device=dev)
-    doff = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    dslot = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    dlen = torch.empty(n, dtype=torch.int64, device=dev)
     dst = torch.empty(n, dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream(dev)
+    from psyne_amd._lib import check
+    lib, h, sp = codec._lib, codec._h, stream.cuda_stream
+    P = lambda t: t.data_ptr()
 
     def step(ev=None):
         if ev:
             ev[0].record(stream)
-        codec.encode_batch(data, off, out=enc, out_offsets=eoff, status=est)
+        check(lib.tdt_encode_slots(h, P(off), n, P(eslot), sp))
+        check(lib.tdt_encode_batch_into(h, P(data), P(off), n, P(enc), P(eslot), P(elen), P(est), sp))
         if ev:
             ev[1].record(stream)
-        codec.decode_batch(enc, eoff, out=dec, out_offsets=doff, status=dst)
+        check(lib.tdt_decode_slots(h, P(enc), P(eslot), P(elen), n, P(dslot), P(dst), sp))
+        check(lib.tdt_decode_batch_into(h, P(enc), P(eslot), P(elen), n, P(dec), P(dslot), P(dlen), P(dst), sp))
         if ev:
             ev[2].record(stream)
 
@@ -154,7 +166,8 @@ def main():
     torch.cuda.synchronize(dev)
     # correctness of the measured configuration (size-independent property): round trip
     ok = bool(torch.equal(dec, data)) and int(est.abs().sum()) == 0 and int(dst.abs().sum()) == 0
-    enc_bytes = int(eoff[-1].item())
+    ok = ok and bool(torch.equal(dslot, off))
+    enc_bytes = int(elen.sum().item())
 
     if world > 1:
         dist.barrier()

@@ -18,6 +18,8 @@
  *                                     blobs made in the reference's random-sample mode)
  *   tdt_decode_batch                  decode                                      :271-304
  *   tdt_decoded_sizes_batch           the output size decode would produce (header parse)
+ *   tdt_encode_batch_into /           encode / decode into caller slots (one vector per
+ *   tdt_decode_batch_into             message, as the reference returns them)
  *   tdt_analyze_batch                 analyze_data / extract_features / perform_clustering
  *                                     :206-222, :434-525 (full-sample histograms, entropies,
  *                                     mapping per message)
@@ -28,7 +30,8 @@
  * 0x554E4350 + payload, or TDT header | mapping | (u32 len, RLE pairs) per stream.
  *
  * Batch layout: message i occupies in[in_off[i] .. in_off[i+1]) (in_off has n+1
- * entries, device memory).  Outputs are COMPACTED: message i's result is written at
+ * entries, device memory).  Outputs are either SLOTTED (the *_into entry points, below) or
+ * COMPACTED (tdt_encode_batch / tdt_decode_batch): message i's result is written at
  * out[out_off[i] .. out_off[i+1]) and the kernel fills out_off (n+1 entries, device
  * memory) itself with a single-pass decoupled look-back, so the caller never needs the
  * sizes up front.  Per-message status codes go to status[i] if status != NULL.
@@ -115,6 +118,28 @@ int tdt_encode_with_mapping_batch(tdt_ctx *ctx, const uint8_t *d_in, const uint6
 int tdt_decode_batch(tdt_ctx *ctx, const uint8_t *d_in, const uint64_t *d_in_off, uint32_t n_msgs,
                      uint8_t *d_out, uint64_t out_cap, uint64_t *d_out_off, int32_t *d_status,
                      void *hip_stream);
+
+/* SLOTTED batches — the hot path.  No dependency between messages: blob i goes to
+ * out[slot_off[i] ..) with capacity slot_off[i+1] - slot_off[i] (slot_off: n+1 entries,
+ * device memory, chosen by the caller — tdt_encode_slots gives the prefix sum of the encode
+ * bounds, tdt_decode_slots the prefix sum of the decoded sizes); its length goes to
+ * out_len[i] (0 with status TDT_E_CAPACITY if the slot is too small).  This is the layout of
+ * the reference's API — one independent vector per message (:227-266, :271-304) — and of
+ * batched GPU codecs generally: each blob is sent as its own frame. */
+int tdt_encode_batch_into(tdt_ctx *ctx, const uint8_t *d_in, const uint64_t *d_in_off, uint32_t n_msgs,
+                          uint8_t *d_out, const uint64_t *d_slot_off, uint64_t *d_out_len, int32_t *d_status,
+                          void *hip_stream);
+/* Decode input: blob i = in[in_off[i] .. in_off[i] + in_len[i]) when d_in_len != NULL (e.g. the
+ * slots and lengths tdt_encode_batch_into produced), else in[in_off[i] .. in_off[i+1]). */
+int tdt_decode_batch_into(tdt_ctx *ctx, const uint8_t *d_in, const uint64_t *d_in_off, const uint64_t *d_in_len,
+                          uint32_t n_msgs, uint8_t *d_out, const uint64_t *d_slot_off, uint64_t *d_out_len,
+                          int32_t *d_status, void *hip_stream);
+/* d_slot_off (n+1 entries) = exclusive prefix sum of tdt_encode_bound(size_i, word_size). */
+int tdt_encode_slots(tdt_ctx *ctx, const uint64_t *d_in_off, uint32_t n_msgs, uint64_t *d_slot_off,
+                     void *hip_stream);
+/* d_slot_off (n+1 entries) = exclusive prefix sum of the decoded sizes (header parse). */
+int tdt_decode_slots(tdt_ctx *ctx, const uint8_t *d_in, const uint64_t *d_in_off, const uint64_t *d_in_len,
+                     uint32_t n_msgs, uint64_t *d_slot_off, int32_t *d_status, void *hip_stream);
 
 /* Decoded size of each blob (0 for blobs with an error status). */
 int tdt_decoded_sizes_batch(tdt_ctx *ctx, const uint8_t *d_in, const uint64_t *d_in_off,

@@ -40,6 +40,10 @@ SIGNATURES = {
     "tdt_encode_with_mapping_batch": (C.c_int, [_vp, _vp, _vp, C.c_uint32, _vp, _vp, C.c_uint64, _vp, _vp, _vp]),
     "tdt_decode_batch": (C.c_int, [_vp, _vp, _vp, C.c_uint32, _vp, C.c_uint64, _vp, _vp, _vp]),
     "tdt_decoded_sizes_batch": (C.c_int, [_vp, _vp, _vp, C.c_uint32, _vp, _vp, _vp]),
+    "tdt_encode_batch_into": (C.c_int, [_vp, _vp, _vp, C.c_uint32, _vp, _vp, _vp, _vp, _vp]),
+    "tdt_decode_batch_into": (C.c_int, [_vp, _vp, _vp, _vp, C.c_uint32, _vp, _vp, _vp, _vp, _vp]),
+    "tdt_encode_slots": (C.c_int, [_vp, _vp, C.c_uint32, _vp, _vp]),
+    "tdt_decode_slots": (C.c_int, [_vp, _vp, _vp, _vp, C.c_uint32, _vp, _vp, _vp]),
     "tdt_analyze_batch": (C.c_int, [_vp, _vp, _vp, C.c_uint32, _vp, _vp, _vp, _vp, _vp]),
     "tdt_encode_host": (C.c_int, [_vp, _vp, _vp, C.c_uint32, _vp, C.c_uint64, _vp, _vp]),
     "tdt_decode_host": (C.c_int, [_vp, _vp, _vp, C.c_uint32, _vp, C.c_uint64, _vp, _vp]),

@@ -17,6 +17,7 @@
 
 #include "tdt_decode.h"
 #include "tdt_encode.h"
+#include "tdt_slots.h"
 
 namespace {
 
@@ -77,27 +78,28 @@ bool policy_on(const tdt_ctx *c) {
            c->bandwidth.load() < c->cfg.bandwidth_threshold_mbps;
 }
 
-template <int WS, int TEAM, int G, int MODE>
+template <int WS, int TEAM, int G, int MODE, int LB>
 int launch_encode_t(psy::EncodeArgs a, hipStream_t s) {
-    hipLaunchKernelGGL((psy::tdt_encode_kernel<WS, TEAM, G, MODE>), dim3(a.n_msgs), dim3(TEAM), 0, s, a);
+    hipLaunchKernelGGL((psy::tdt_encode_kernel<WS, TEAM, G, MODE, LB>), dim3(a.n_msgs), dim3(TEAM), 0, s, a);
     return TDT_OK;
 }
 
-template <int WS, int MODE>
+template <int WS, int MODE, int LB>
 int launch_encode_ws(psy::EncodeArgs a, bool small, hipStream_t s) {
-    if (small) return launch_encode_t<WS, 64, 4, MODE>(a, s);
-    return launch_encode_t<WS, 256, 16, MODE>(a, s);
+    if (small) return launch_encode_t<WS, 64, 4, MODE, LB>(a, s);
+    return launch_encode_t<WS, 512, 8, MODE, LB>(a, s);
 }
 
-template <int MODE>
+// LB: compacted output (look-back) vs slotted output
+template <int MODE, int LB>
 int launch_encode(tdt_ctx *c, psy::EncodeArgs a, hipStream_t s) {
     const bool small = c->size_hint.load() <= 4096;
     switch (c->cfg.word_size) {
-        case 1: return launch_encode_ws<1, MODE>(a, small, s);
-        case 2: return launch_encode_ws<2, MODE>(a, small, s);
-        case 4: return launch_encode_ws<4, MODE>(a, small, s);
-        case 8: return launch_encode_ws<8, MODE>(a, small, s);
-        case 16: return launch_encode_ws<16, MODE>(a, small, s);
+        case 1: return launch_encode_ws<1, MODE, LB>(a, small, s);
+        case 2: return launch_encode_ws<2, MODE, LB>(a, small, s);
+        case 4: return launch_encode_ws<4, MODE, LB>(a, small, s);
+        case 8: return launch_encode_ws<8, MODE, LB>(a, small, s);
+        case 16: return launch_encode_ws<16, MODE, LB>(a, small, s);
     }
     return set_err(TDT_E_UNSUPPORTED, "word_size not supported on the GPU path");
 }
@@ -112,11 +114,13 @@ int prep(tdt_ctx *c, uint32_t n_msgs, hipStream_t s) {
 
 int encode_common(tdt_ctx *c, int mode, const uint8_t *d_in, const uint64_t *d_in_off, uint32_t n_msgs,
                   const int32_t *d_mapping, uint8_t *d_out, uint64_t out_cap, uint64_t *d_out_off,
-                  int32_t *d_status, uint32_t *d_hist, double *d_ent, int32_t *d_map, void *stream) {
+                  int32_t *d_status, uint32_t *d_hist, double *d_ent, int32_t *d_map, void *stream,
+                  const uint64_t *d_slot_off = nullptr, uint64_t *d_out_len = nullptr) {
     if (!c) return set_err(TDT_E_ARG, "null context");
     if (n_msgs == 0) return TDT_OK;
     if (!d_in_off) return set_err(TDT_E_ARG, "null input offsets");  // d_in may be null: all-empty batch
-    if (mode != psy::MODE_ANALYZE && (!d_out || !d_out_off)) return set_err(TDT_E_ARG, "null output");
+    const bool slotted = d_slot_off != nullptr;
+    if (mode != psy::MODE_ANALYZE && (!d_out || (!slotted && !d_out_off))) return set_err(TDT_E_ARG, "null output");
     if (mode == psy::MODE_MAPPED && !d_mapping) return set_err(TDT_E_ARG, "null mapping");
     hipStream_t s = (hipStream_t)stream;
     std::lock_guard<std::mutex> lk(c->mu);
@@ -139,9 +143,15 @@ int encode_common(tdt_ctx *c, int mode, const uint8_t *d_in, const uint64_t *d_i
     a.lookback = reinterpret_cast<uint64_t *>(c->ws + kCounterBytes);
     a.min_tensor = c->cfg.min_tensor_size;
     a.policy_on = policy_on(c) ? 1 : 0;
-    if (mode == psy::MODE_ENCODE) st = launch_encode<psy::MODE_ENCODE>(c, a, s);
-    else if (mode == psy::MODE_MAPPED) st = launch_encode<psy::MODE_MAPPED>(c, a, s);
-    else st = launch_encode<psy::MODE_ANALYZE>(c, a, s);
+    a.slot_off = d_slot_off;
+    a.out_len = d_out_len;
+    if (mode == psy::MODE_ENCODE) {
+        st = slotted ? launch_encode<psy::MODE_ENCODE, 0>(c, a, s) : launch_encode<psy::MODE_ENCODE, 1>(c, a, s);
+    } else if (mode == psy::MODE_MAPPED) {
+        st = launch_encode<psy::MODE_MAPPED, 1>(c, a, s);
+    } else {
+        st = launch_encode<psy::MODE_ANALYZE, 1>(c, a, s);
+    }
     if (st) return st;
     HIPCHK(hipGetLastError());
     return TDT_OK;
@@ -149,11 +159,13 @@ int encode_common(tdt_ctx *c, int mode, const uint8_t *d_in, const uint64_t *d_i
 
 int decode_common(tdt_ctx *c, bool sizes_only, const uint8_t *d_in, const uint64_t *d_in_off, uint32_t n_msgs,
                   uint8_t *d_out, uint64_t out_cap, uint64_t *d_out_off, uint64_t *d_sizes, int32_t *d_status,
-                  void *stream) {
+                  void *stream, const uint64_t *d_slot_off = nullptr, uint64_t *d_out_len = nullptr,
+                  const uint64_t *d_in_len = nullptr) {
     if (!c) return set_err(TDT_E_ARG, "null context");
     if (n_msgs == 0) return TDT_OK;
     if (!d_in_off) return set_err(TDT_E_ARG, "null input offsets");
-    if (!sizes_only && (!d_out_off)) return set_err(TDT_E_ARG, "null output offsets");
+    const bool slotted = d_slot_off != nullptr;
+    if (!sizes_only && !slotted && !d_out_off) return set_err(TDT_E_ARG, "null output offsets");
     if (sizes_only && !d_sizes) return set_err(TDT_E_ARG, "null sizes");
     hipStream_t s = (hipStream_t)stream;
     std::lock_guard<std::mutex> lk(c->mu);
@@ -171,13 +183,18 @@ int decode_common(tdt_ctx *c, bool sizes_only, const uint8_t *d_in, const uint64
     a.ticket = reinterpret_cast<uint32_t *>(c->ws);
     a.errflags = reinterpret_cast<uint32_t *>(c->ws) + 1;
     a.lookback = reinterpret_cast<uint64_t *>(c->ws + kCounterBytes);
+    a.slot_off = d_slot_off;
+    a.out_len = d_out_len;
+    a.in_len = d_in_len;
     const bool small = c->size_hint.load() <= 4096;
     if (sizes_only) {
-        hipLaunchKernelGGL((psy::tdt_decode_kernel<64, 1>), dim3(n_msgs), dim3(64), 0, s, a);
+        hipLaunchKernelGGL((psy::tdt_decode_kernel<64, 1, 1>), dim3(n_msgs), dim3(64), 0, s, a);
     } else if (small) {
-        hipLaunchKernelGGL((psy::tdt_decode_kernel<64, 0>), dim3(n_msgs), dim3(64), 0, s, a);
+        if (slotted) hipLaunchKernelGGL((psy::tdt_decode_kernel<64, 0, 0>), dim3(n_msgs), dim3(64), 0, s, a);
+        else hipLaunchKernelGGL((psy::tdt_decode_kernel<64, 0, 1>), dim3(n_msgs), dim3(64), 0, s, a);
     } else {
-        hipLaunchKernelGGL((psy::tdt_decode_kernel<256, 0>), dim3(n_msgs), dim3(256), 0, s, a);
+        if (slotted) hipLaunchKernelGGL((psy::tdt_decode_kernel<256, 0, 0>), dim3(n_msgs), dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((psy::tdt_decode_kernel<256, 0, 1>), dim3(n_msgs), dim3(256), 0, s, a);
     }
     HIPCHK(hipGetLastError());
     return TDT_OK;
@@ -339,6 +356,48 @@ int tdt_decode_batch(tdt_ctx *ctx, const uint8_t *d_in, const uint64_t *d_in_off
 int tdt_decoded_sizes_batch(tdt_ctx *ctx, const uint8_t *d_in, const uint64_t *d_in_off, uint32_t n_msgs,
                             uint64_t *d_sizes, int32_t *d_status, void *stream) {
     return decode_common(ctx, true, d_in, d_in_off, n_msgs, nullptr, 0, nullptr, d_sizes, d_status, stream);
+}
+
+int tdt_encode_batch_into(tdt_ctx *ctx, const uint8_t *d_in, const uint64_t *d_in_off, uint32_t n_msgs,
+                          uint8_t *d_out, const uint64_t *d_slot_off, uint64_t *d_out_len, int32_t *d_status,
+                          void *stream) {
+    if (n_msgs && !d_slot_off) return set_err(TDT_E_ARG, "null slot offsets");
+    return encode_common(ctx, psy::MODE_ENCODE, d_in, d_in_off, n_msgs, nullptr, d_out, 0, nullptr, d_status, nullptr,
+                         nullptr, nullptr, stream, d_slot_off, d_out_len);
+}
+
+int tdt_decode_batch_into(tdt_ctx *ctx, const uint8_t *d_in, const uint64_t *d_in_off, const uint64_t *d_in_len,
+                          uint32_t n_msgs, uint8_t *d_out, const uint64_t *d_slot_off, uint64_t *d_out_len,
+                          int32_t *d_status, void *stream) {
+    if (n_msgs && !d_slot_off) return set_err(TDT_E_ARG, "null slot offsets");
+    return decode_common(ctx, false, d_in, d_in_off, n_msgs, d_out, 0, nullptr, nullptr, d_status, stream, d_slot_off,
+                         d_out_len, d_in_len);
+}
+
+int tdt_encode_slots(tdt_ctx *ctx, const uint64_t *d_in_off, uint32_t n_msgs, uint64_t *d_slot_off, void *stream) {
+    if (!ctx) return set_err(TDT_E_ARG, "null context");
+    if (!d_slot_off || (n_msgs && !d_in_off)) return set_err(TDT_E_ARG, "null offsets");
+    HIPCHK(hipSetDevice(ctx->device));
+    hipLaunchKernelGGL((psy::tdt_slots_kernel<0>), dim3(1), dim3(1024), 0, (hipStream_t)stream, d_in_off, d_slot_off,
+                       n_msgs, (uint32_t)ctx->cfg.word_size);
+    HIPCHK(hipGetLastError());
+    return TDT_OK;
+}
+
+int tdt_decode_slots(tdt_ctx *ctx, const uint8_t *d_in, const uint64_t *d_in_off, const uint64_t *d_in_len,
+                     uint32_t n_msgs, uint64_t *d_slot_off, int32_t *d_status, void *stream) {
+    if (!ctx) return set_err(TDT_E_ARG, "null context");
+    if (!d_slot_off) return set_err(TDT_E_ARG, "null offsets");
+    if (n_msgs) {
+        int st = decode_common(ctx, true, d_in, d_in_off, n_msgs, nullptr, 0, nullptr, d_slot_off, d_status, stream,
+                               nullptr, nullptr, d_in_len);
+        if (st) return st;
+    }
+    HIPCHK(hipSetDevice(ctx->device));
+    hipLaunchKernelGGL((psy::tdt_slots_kernel<1>), dim3(1), dim3(1024), 0, (hipStream_t)stream, d_in_off, d_slot_off,
+                       n_msgs, 0u);
+    HIPCHK(hipGetLastError());
+    return TDT_OK;
 }
 
 int tdt_encode_host(tdt_ctx *ctx, const uint8_t *h_in, const uint64_t *h_in_off, uint32_t n_msgs, uint8_t *h_out,

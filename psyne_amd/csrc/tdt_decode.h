@@ -32,6 +32,9 @@ struct DecodeArgs {
     uint64_t *lookback;
     uint32_t *ticket;
     uint32_t *errflags;
+    const uint64_t *slot_off;  // slotted outputs (LB = 0)
+    const uint64_t *in_len;    // optional blob lengths (blob i = in[in_off[i] .. +in_len[i]))
+    uint64_t *out_len;
 };
 
 constexpr int kMaxRef = 16;  // referenced streams <= word_size <= 16
@@ -54,7 +57,7 @@ struct DecLayout {
 enum { D_MSG = 0, D_STATUS = 1, D_UNCP = 2, D_ORIG = 3, D_WS = 4, D_NREF = 5, D_BASE = 6,
        D_K = 8, D_SOFF = 24, D_NP = 40, D_SEL = 56, D_PIDX = 184, D_POS = 200, D_CARRY = 216 };
 
-template <int TEAM, int SIZES_ONLY>
+template <int TEAM, int SIZES_ONLY, int LB>
 __global__ __launch_bounds__(TEAM) void tdt_decode_kernel(DecodeArgs a) {
     using Lay = DecLayout<TEAM>;
     constexpr int W = Lay::W;
@@ -70,7 +73,7 @@ __global__ __launch_bounds__(TEAM) void tdt_decode_kernel(DecodeArgs a) {
     const uint32_t msg = __builtin_amdgcn_readfirstlane(misc[D_MSG]);
     if (msg >= a.n_msgs) return;
     const uint64_t boff = a.in_off[msg];
-    const uint64_t len = a.in_off[msg + 1] - boff;
+    const uint64_t len = a.in_len ? a.in_len[msg] : a.in_off[msg + 1] - boff;
     const uint8_t *blob = a.in + boff;
 
     // ------------------------------------------------ header parse (thread 0)
@@ -182,19 +185,39 @@ __global__ __launch_bounds__(TEAM) void tdt_decode_kernel(DecodeArgs a) {
             a.sizes_out[msg] = osize;
             if (a.status) a.status[msg] = (int32_t)st;
         } else {
-            const uint64_t b = lookback_excl(a.lookback, msg, osize, a.errflags);
+            *reinterpret_cast<uint64_t *>(misc + D_BASE) = osize;
+        }
+    }
+    if constexpr (SIZES_ONLY) return;
+    team_sync<W>();
+    if (tid < 64) {  // wave 0: output placement (look-back on the decoded size, or slot)
+        const uint64_t osize = *reinterpret_cast<const uint64_t *>(misc + D_BASE);
+        uint64_t b;
+        bool fits;
+        if constexpr (LB) {
+            b = lookback_excl_wave(a.lookback, msg, osize, a.errflags);
+            fits = b + osize <= a.out_cap;
+        } else {
+            b = a.slot_off[msg];
+            fits = osize <= a.slot_off[msg + 1] - b;
+        }
+        if (tid == 0) {
+            uint32_t st = misc[D_STATUS];
             *reinterpret_cast<uint64_t *>(misc + D_BASE) = b;
-            const bool fits = b + osize <= a.out_cap;
-            a.out_off[msg] = b;
-            if (msg == a.n_msgs - 1) a.out_off[a.n_msgs] = b + osize;
+            if constexpr (LB) {
+                a.out_off[msg] = b;
+                if (msg == a.n_msgs - 1) a.out_off[a.n_msgs] = b + osize;
+            }
             if (st == ST_OK && !fits) {
                 st = ST_CAPACITY;
                 misc[D_STATUS] = st;
             }
+            if constexpr (!LB) {
+                if (a.out_len) a.out_len[msg] = st == ST_OK ? osize : 0;
+            }
             if (a.status) a.status[msg] = (int32_t)st;
         }
     }
-    if constexpr (SIZES_ONLY) return;
     team_sync<W>();
     const uint32_t st = __builtin_amdgcn_readfirstlane(misc[D_STATUS]);
     if (st != ST_OK) return;

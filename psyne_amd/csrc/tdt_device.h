@@ -194,6 +194,74 @@ __device__ __forceinline__ uint64_t lookback_excl(uint64_t *st, uint32_t i, uint
     return excl;
 }
 
+// Sum of a u64 over the wave (butterfly on both 32-bit halves).
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
+#pragma unroll
+    for (int o = 32; o; o >>= 1) {
+        const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, o);
+        const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), o);
+        v += ((uint64_t)hi << 32) | lo;
+    }
+    return v;
+}
+
+// Wave-parallel look-back: called by ALL lanes of one wave (uniform control flow); returns
+// the exclusive prefix of message i in every lane.  Each round trip reads the 64 status
+// words below the window's top at once; the nearest inclusive prefix (a ballot) ends the
+// walk, windows of aggregates are summed and skipped, a window with an unpublished word is
+// re-read.  Message indices below 0 read as "inclusive 0".  Bounded spin as above.
+__device__ __forceinline__ uint64_t lookback_excl_wave(uint64_t *st, uint32_t i, uint64_t agg,
+                                                       uint32_t *timeout) {
+    const int lane = lane_id();
+    if (i == 0) {
+        if (lane == 0) lb_store(&st[0], kLbInc | agg);
+        return 0;
+    }
+    if (lane == 0) lb_store(&st[i], kLbAgg | agg);
+    uint64_t excl = 0;
+    int64_t top = (int64_t)i;  // window [top - 64, top)
+    uint32_t spins = 0;
+    while (true) {
+        const int64_t j = top - 64 + lane;
+        const uint64_t s = j >= 0 ? lb_load(&st[j]) : kLbInc;
+        const uint32_t f = (uint32_t)(s >> 62);
+        const uint64_t bz = __ballot(f == 0);
+        const uint64_t bp = __ballot(f == 2);
+        uint64_t need;  // lanes whose value is part of the prefix
+        if (bp) {
+            const int hp = 63 - __builtin_clzll(bp);
+            need = ~0ull << hp;
+        } else {
+            need = ~0ull;
+        }
+        if (bz & need) {
+#if defined(PSY_PROF) && PSY_PROF
+            if (lane == 0) atomicAdd(&psy_prof[16], 1ull);
+#endif
+            if (++spins > (1u << 24)) {
+                if (lane == 0) atomicOr(timeout, 1u);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        excl += wave_sum_u64(((need >> lane) & 1ull) ? (s & kLbVal) : 0ull);
+#if defined(PSY_PROF) && PSY_PROF
+        if (lane == 0) atomicAdd(&psy_prof[17], 1ull);
+#endif
+        if (bp) break;
+        top -= 64;
+    }
+    if (lane == 0) lb_store(&st[i], kLbInc | (excl + agg));
+#if defined(PSY_PROF) && PSY_PROF
+    if (lane == 0) {
+        atomicAdd(&psy_prof[18], 1ull);
+        if (spins) atomicAdd(&psy_prof[19], 1ull);
+    }
+#endif
+    return excl;
+}
+
 // ---------------------------------------------------------------------------------------
 // Byte-exact accesses.
 __device__ __forceinline__ uint32_t ld_u8(const uint8_t *p) { return *p; }

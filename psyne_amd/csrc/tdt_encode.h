@@ -15,7 +15,8 @@
 // claimed through an atomic ticket.  A message is a sequence of 16-byte GROUPS.  Wave w owns
 // the contiguous group range [w·RW·64, (w+1)·RW·64); round r of the wave is one coalesced
 // 1 KiB sweep (lane l ↔ group (w·RW + r)·64 + l).  Messages of up to G rounds per wave stay
-// in VGPRs across all passes (the round arrays are rotated, never dynamically indexed).
+// in VGPRs across all passes: the resident round loops are fully unrolled (compile-time
+// array indices, no register moves); pass A1 replaces each round's bytes by its slot word T.
 //
 // Both streams of a group live in ONE 16-slot word — stream 0 in slots [0, L0), stream 1 in
 // [L0, 16) — transposed so that slot j = 4t + q is byte t of dword q: the byte before slot j
@@ -69,6 +70,8 @@ struct EncodeArgs {
     uint64_t *lookback;
     uint32_t *ticket;
     uint32_t *errflags;  // bit0 look-back timeout, bit2 flush bound
+    const uint64_t *slot_off;  // slotted outputs (LB = 0): blob i at out + slot_off[i]
+    uint64_t *out_len;         // slotted outputs: blob lengths
     uint64_t min_tensor;
     int32_t policy_on;  // bandwidth < threshold && cpu <= threshold (host-evaluated atomics)
 };
@@ -85,7 +88,7 @@ struct EncLayout {
     static constexpr int TB = (TEAM >= 256) ? (WS < 4 ? WS : 4) : (WS < 2 ? WS : 2);
     // one stream's pairs of one wave-round: alignment pad + 1024 pairs + one garbage pair
     static constexpr int WREGION = 16 + 2 * 64 * 16 + 16;
-    static constexpr int WSTAGE = 2 * WREGION;  // both streams, per wave
+    static constexpr int WSTAGE = 2 * WREGION + 16;  // both streams + a junk pair, per wave
     static constexpr int STAGE = W * WSTAGE;
     static constexpr int TERMS = TB * 256 * 16;
     static constexpr int UNION = STAGE > TERMS ? STAGE : TERMS;
@@ -128,7 +131,10 @@ __device__ __forceinline__ uint32_t spread2(uint32_t e) {
     return x | (x << 1);
 }
 
-template <int WS, int TEAM, int G, int MODE>
+// LB = 1: compacted output, offsets by decoupled look-back (out_off written);
+// LB = 0: slotted output at caller offsets (slot_off), lengths to out_len — no dependency
+//         between messages.
+template <int WS, int TEAM, int G, int MODE, int LB>
 __global__ __launch_bounds__(TEAM) void tdt_encode_kernel(EncodeArgs a) {
     using Lay = EncLayout<WS, TEAM>;
     constexpr int W = Lay::W;
@@ -151,6 +157,30 @@ __global__ __launch_bounds__(TEAM) void tdt_encode_kernel(EncodeArgs a) {
     const uint64_t n = a.in_off[msg + 1] - off0;
     const uint8_t *base = a.in + off0;
 
+    // Output placement of an E-byte result (all threads call it): returns the offset in
+    // a.out and whether the result fits.
+    auto place = [&](uint64_t E, bool &fits) __attribute__((always_inline)) -> uint64_t {
+        uint64_t ob;
+        if constexpr (LB) {
+            if (wv == 0) {
+                const uint64_t b = lookback_excl_wave(a.lookback, msg, E, a.errflags);
+                if (lane == 0) *reinterpret_cast<uint64_t *>(misc + M_BASE) = b;
+            }
+            team_sync<W>();
+            ob = *reinterpret_cast<uint64_t *>(misc + M_BASE);
+            fits = ob + E <= a.out_cap;
+            if (tid == 0) {
+                a.out_off[msg] = ob;
+                if (msg == a.n_msgs - 1) a.out_off[a.n_msgs] = ob + E;
+            }
+        } else {
+            ob = a.slot_off[msg];
+            fits = E <= a.slot_off[msg + 1] - ob;
+            if (tid == 0 && a.out_len) a.out_len[msg] = fits ? E : 0;
+        }
+        return ob;
+    };
+
     bool compress;
     if constexpr (MODE == MODE_ANALYZE) {
         compress = (n > 0) && (n % WS == 0) && (n < (1ull << 32));
@@ -168,18 +198,9 @@ __global__ __launch_bounds__(TEAM) void tdt_encode_kernel(EncodeArgs a) {
     if (!compress) {
         if constexpr (MODE != MODE_ANALYZE) {
             const uint64_t E = n + 4;
-            if (tid == 0) {
-                uint64_t b = lookback_excl(a.lookback, msg, E, a.errflags);
-                *reinterpret_cast<uint64_t *>(misc + M_BASE) = b;
-            }
-            team_sync<W>();
-            const uint64_t ob = *reinterpret_cast<uint64_t *>(misc + M_BASE);
-            const bool fits = ob + E <= a.out_cap;
-            if (tid == 0) {
-                a.out_off[msg] = ob;
-                if (msg == a.n_msgs - 1) a.out_off[a.n_msgs] = ob + E;
-                if (a.status) a.status[msg] = fits ? ST_OK : ST_CAPACITY;
-            }
+            bool fits;
+            const uint64_t ob = place(E, fits);
+            if (tid == 0 && a.status) a.status[msg] = fits ? ST_OK : ST_CAPACITY;
             if (fits) {
                 uint8_t *dst = a.out + ob;
                 if (tid < 4) dst[tid] = (uint8_t)(kMagicUNCP >> (8 * tid));
@@ -215,30 +236,26 @@ __global__ __launch_bounds__(TEAM) void tdt_encode_kernel(EncodeArgs a) {
     // Resident messages keep their RW <= G rounds in VGPRs.  The round loop ROTATES the
     // arrays (compile-time indices only) instead of indexing them with the round number,
     // which would push them to scratch.
-    uint4 dres[G];
+    uint4 dres[G];     // the round's 16 bytes per lane; after pass A1 its slot word T
     uint32_t cres[G];  // run-start masks (A1 → A2), then chunk-start masks (A2 → B)
 #pragma unroll
     for (int r = 0; r < G; ++r) {
         dres[r] = (resident && (uint32_t)r < RW) ? load_group(gw0 + r * 64 + lane) : make_uint4(0, 0, 0, 0);
         cres[r] = 0;
     }
-    auto rotate = [&]() __attribute__((always_inline)) {
-        const uint4 t = dres[0];
-        const uint32_t c = cres[0];
-#pragma unroll
-        for (int q = 0; q < G - 1; ++q) {
-            dres[q] = dres[q + 1];
-            cres[q] = cres[q + 1];
-        }
-        dres[G - 1] = t;
-        cres[G - 1] = c;
-    };
-    // body(r, data, cres&) for every round r < RW of this wave, in order
+    // body(r, data&, cres&, resident) for every round r < RW of this wave, in order.  Resident
+    // rounds: unrolled, compile-time indices; otherwise the round is loaded from HBM.
     auto for_rounds = [&](auto &&body) __attribute__((always_inline)) {
-        const uint32_t iters = resident ? (uint32_t)G : RW;
-        for (uint32_t r = 0; r < iters; ++r) {
-            if (r < RW) body(r, resident ? dres[0] : load_group(gw0 + r * 64 + lane), cres[0]);
-            if (resident) rotate();
+        if (resident) {
+#pragma unroll
+            for (int r = 0; r < G; ++r)
+                if ((uint32_t)r < RW) body((uint32_t)r, dres[r], cres[r], std::true_type{});
+        } else {
+            for (uint32_t r = 0; r < RW; ++r) {
+                uint4 d = load_group(gw0 + r * 64 + lane);
+                uint32_t c = 0;
+                body(r, d, c, std::false_type{});
+            }
         }
     };
 
@@ -256,12 +273,9 @@ __global__ __launch_bounds__(TEAM) void tdt_encode_kernel(EncodeArgs a) {
         team_sync<W>();
         if (misc[M_STATUS]) {
             // invalid caller mapping: publish an empty output for this message
-            if (tid == 0) {
-                uint64_t b = lookback_excl(a.lookback, msg, 0, a.errflags);
-                a.out_off[msg] = b;
-                if (msg == a.n_msgs - 1) a.out_off[a.n_msgs] = b;
-                if (a.status) a.status[msg] = ST_BAD_MAPPING;
-            }
+            bool fits;
+            (void)place(0, fits);
+            if (tid == 0 && a.status) a.status[msg] = ST_BAD_MAPPING;
             return;
         }
     } else {
@@ -284,7 +298,7 @@ __global__ __launch_bounds__(TEAM) void tdt_encode_kernel(EncodeArgs a) {
                     atomicAdd(reinterpret_cast<uint32_t *>(smem + Lay::OFF_HIST + (i % WS) * Lay::PS * 4 + ad), 1u);
             }
         };
-        for_rounds([&](uint32_t r, const uint4 d, uint32_t &) __attribute__((always_inline)) {
+        for_rounds([&](uint32_t r, uint4 &d, uint32_t &, auto) __attribute__((always_inline)) {
             if (full_round(r)) hist_group(d, 16, true);
             else hist_group(d, vbytes(gw0 + r * 64 + lane), false);
         });
@@ -434,6 +448,14 @@ __global__ __launch_bounds__(TEAM) void tdt_encode_kernel(EncodeArgs a) {
         }
         const uint32_t edA = __builtin_amdgcn_readfirstlane(misc[M_EDA]);
         const uint32_t edB = __builtin_amdgcn_readfirstlane(misc[M_EDB]);
+        // selectors extracting slot L0 (stream 1's first byte) from T: slot j is byte j/4 of
+        // T[j%4], i.e. byte (j%4 & 1)*4 + j/4 of perm(T[1],T[0]) or perm(T[3],T[2])
+        uint32_t fsA = 0x0c0c0c0cu, fsB = 0x0c0c0c0cu;
+        if (ns2) {
+            const uint32_t q = L0 & 3u, t = L0 >> 2, sel = 0x0c0c0c00u | ((q & 1u) * 4u + t);
+            if (q < 2) fsA = sel;
+            else fsB = sel;
+        }
         PSY_PROF_MARK(2);
 
         auto tmat = [&](const uint4 &d, uint32_t (&T)[4]) __attribute__((always_inline)) {
@@ -533,7 +555,7 @@ __global__ __launch_bounds__(TEAM) void tdt_encode_kernel(EncodeArgs a) {
         uint32_t wmax[2] = {0, 0};
         {
             uint32_t edc = edc0;
-            for_rounds([&](uint32_t r, const uint4 d, uint32_t &cm) __attribute__((always_inline)) {
+            for_rounds([&](uint32_t r, uint4 &d, uint32_t &cm, auto res) __attribute__((always_inline)) {
                 const uint32_t g = gw0 + r * 64 + lane;
                 uint32_t T[4];
                 tmat(d, T);
@@ -542,6 +564,7 @@ __global__ __launch_bounds__(TEAM) void tdt_encode_kernel(EncodeArgs a) {
                 const uint32_t m = run_mask(T, ed, edc, g, V);
                 edc = rdlane(ed, 63);
                 cm = m;
+                if constexpr (decltype(res)::value) d = make_uint4(T[0], T[1], T[2], T[3]);
                 const uint32_t m0 = m & lowL0;
                 if (m0) wmax[0] = umax(wmax[0], g * Ls[0] + hibit(m0) + 1u);
                 if (ns2) {
@@ -574,11 +597,11 @@ __global__ __launch_bounds__(TEAM) void tdt_encode_kernel(EncodeArgs a) {
         {
             uint32_t rcarry[2] = {rin[0], rin[1]};
             uint32_t edc = edc0;
-            for_rounds([&](uint32_t r, const uint4 d, uint32_t &cm) __attribute__((always_inline)) {
+            for_rounds([&](uint32_t r, uint4 &d, uint32_t &cm, auto res) __attribute__((always_inline)) {
                 const uint32_t g = gw0 + r * 64 + lane;
                 const uint32_t V = full_round(r) ? 0xffffu : vmask(vbytes(g));
                 uint32_t m;
-                if (resident) {
+                if constexpr (decltype(res)::value) {
                     m = cm;
                 } else {
                     uint32_t T[4];
@@ -619,18 +642,9 @@ __global__ __launch_bounds__(TEAM) void tdt_encode_kernel(EncodeArgs a) {
         const uint32_t P1 = ns2 ? __builtin_amdgcn_readfirstlane(ptot[1]) : 0u;
         const uint32_t hdr = 20 + 4 * WS;
         const uint64_t E = hdr + (4 + 2ull * P0) + (ns2 ? 4 + 2ull * P1 : 0);
-        if (tid == 0) {
-            uint64_t b = lookback_excl(a.lookback, msg, E, a.errflags);
-            *reinterpret_cast<uint64_t *>(misc + M_BASE) = b;
-        }
-        team_sync<W>();
-        const uint64_t ob = *reinterpret_cast<uint64_t *>(misc + M_BASE);
-        const bool fits = ob + E <= a.out_cap;
-        if (tid == 0) {
-            a.out_off[msg] = ob;
-            if (msg == a.n_msgs - 1) a.out_off[a.n_msgs] = ob + E;
-            if (a.status) a.status[msg] = fits ? ST_OK : ST_CAPACITY;
-        }
+        bool fits;
+        const uint64_t ob = place(E, fits);
+        if (tid == 0 && a.status) a.status[msg] = fits ? ST_OK : ST_CAPACITY;
         if (!fits) return;
         // header :84-106 and stream length words :110-112
         uint8_t *dst = a.out + ob;
@@ -670,16 +684,14 @@ __global__ __launch_bounds__(TEAM) void tdt_encode_kernel(EncodeArgs a) {
             }
         }
 
-        // Emit the pairs of round r: d its data, C its chunk-start mask, nxt63 the chunk bits
-        // of the group after lane 63's (combined layout).
-        auto emit = [&](uint32_t r, const uint4 &d, uint32_t C, uint32_t nxt63) __attribute__((always_inline)) {
+        // Emit the pairs of round r: Tw its slot word, C its chunk-start mask, nxt63 the chunk
+        // bits of the group after lane 63's (combined layout).
+        auto emit = [&](uint32_t r, const uint4 &Tw, uint32_t C, uint32_t nxt63) __attribute__((always_inline)) {
+            const uint32_t T[4] = {Tw.x, Tw.y, Tw.z, Tw.w};
             const uint32_t g = gw0 + r * 64 + lane;
             // the message does not end inside (or before the end of) this round
             const bool inner = 16ull * (gw0 + r * 64 + 64) < n;
             const uint32_t V = inner ? 0xffffu : vmask(vbytes(g));
-            uint32_t T[4];
-            tmat(d, T);
-            const uint32_t ed = edges(d);
             const uint32_t rb[2] = {(gw0 + r * 64) * Ls[0], (gw0 + r * 64) * Ls[1]};
             // last chunk start + 1 before each group (packed, round-relative; 0 = earlier)
             const uint32_t cinc = wave_incl_scan<OpPkMax>(last_starts(C));
@@ -719,63 +731,50 @@ __global__ __launch_bounds__(TEAM) void tdt_encode_kernel(EncodeArgs a) {
                 const uint32_t fi = pr[c] + ((pexc >> (16 * c)) & 0xffffu) - (((C >> off) & 1u) ? 0u : 1u);
                 base[c] = rbs[c] + 2u * (fi - k0c[c]);
             }
+            // Lanes past the message end write into the wave's junk pair.  Every other slot
+            // that is not a chunk END writes where a later write of the same lane (its chunk's
+            // END slot, ascending order), the repair below, or nothing that is flushed (index
+            // >= ends: the slots after a lane's last END in the final group) overwrites it.
+            if (!inner && V == 0) base[0] = base[1] = wst + 2u * Lay::WREGION;
             const uint32_t E2 = spread2(e);
             const uint32_t base1p = base[1] - 2u * popc(e & lowL0);
-            // sweep 1: every valid slot, ascending
-            auto sweep = [&](auto odd) __attribute__((always_inline)) {
+            // sweep 1: every slot, ascending; count = distance to the last chunk start <= j
 #pragma unroll
-                for (int j = 0; j < 16; j += 2) {
-                    const int q = j & 3, t = j >> 2;
-                    const uint32_t ca = ffbh_u32(C << (31 - j)), cb = ffbh_u32(C << (30 - j));
-                    const uint32_t pair = (perm(cb, ca, 0x0c040c00u) + 0x00010001u) |
-                                          perm(T[q + 1], T[q], 0x0cu | ((uint32_t)t << 8) | (0x0cu << 16) |
-                                                                   ((uint32_t)(4 + t) << 24));
+            for (int j = 0; j < 16; j += 2) {
+                const int q = j & 3, t = j >> 2;
+                const uint32_t ca = ffbh_u32(C << (31 - j)), cb = ffbh_u32(C << (30 - j));
+                const uint32_t pair =
+                    (perm(cb, ca, 0x0c040c00u) + 0x00010001u) |
+                    perm(T[q + 1], T[q], 0x0cu | ((uint32_t)t << 8) | (0x0cu << 16) | ((uint32_t)(4 + t) << 24));
 #pragma unroll
-                    for (int h = 0; h < 2; ++h) {
-                        const int jj = j + h;
-                        const uint32_t ad = ((uint32_t)jj < L0 ? base[0] : base1p) +
-                                            (jj ? popc(E2 & ((1u << (2 * jj)) - 1u)) : 0u);
-                        const uint32_t pv = h ? (pair >> 16) : (pair & 0xffffu);
-                        if (inner || ((V >> jj) & 1u)) {
-                            if constexpr (decltype(odd)::value) {
-                                smem[ad] = (uint8_t)pv;
-                                smem[ad + 1] = (uint8_t)(pv >> 8);
-                            } else {
-                                *reinterpret_cast<uint16_t *>(smem + ad) = (uint16_t)pv;
-                            }
-                        }
-                    }
+                for (int h = 0; h < 2; ++h) {
+                    const int jj = j + h;
+                    const uint32_t ad = ((uint32_t)jj < L0 ? base[0] : base1p) +
+                                        (jj ? popc(E2 & ((1u << (2 * jj)) - 1u)) : 0u);
+                    *reinterpret_cast<uint16_t *>(smem + ad) = (uint16_t)(h ? (pair >> 16) : pair);
                 }
-                // sweep 2: the first pair ending in this group, per stream (its chunk may have
-                // begun in an earlier group; also repairs same-instruction collisions)
+            }
+            // sweep 2: the first pair ending in this group, per stream (its chunk may have begun
+            // in an earlier group; this also repairs same-instruction collisions)
 #pragma unroll
-                for (int c = 0; c < 2; ++c) {
-                    if (Ls[c] == 0) continue;
-                    const uint32_t off = c ? L0 : 0u;
-                    const uint32_t ec = c ? (e >> L0) : (e & lowL0);
-                    if (ec) {
-                        const uint32_t jf = lobit(ec);
-                        uint32_t cnt;
-                        if ((C >> off) & 1u) {
-                            cnt = jf + 1u;
-                        } else {
-                            const uint32_t cer = (cexc >> (16 * c)) & 0xffffu;
-                            const uint32_t lcp = cer ? rb[c] + cer : ccarry[c];  // last chunk start + 1
-                            cnt = g * Ls[c] + jf + 2u - lcp;
-                        }
-                        const uint32_t val = c ? ((ed >> 16) & 0xffu) : (T[0] & 0xffu);
-                        const uint32_t pv = (cnt & 0xffu) | (val << 8);
-                        if constexpr (decltype(odd)::value) {
-                            smem[base[c]] = (uint8_t)pv;
-                            smem[base[c] + 1] = (uint8_t)(pv >> 8);
-                        } else {
-                            *reinterpret_cast<uint16_t *>(smem + base[c]) = (uint16_t)pv;
-                        }
+            for (int c = 0; c < 2; ++c) {
+                if (Ls[c] == 0) continue;
+                const uint32_t off = c ? L0 : 0u;
+                const uint32_t ec = c ? (e >> L0) : (e & lowL0);
+                if (ec) {
+                    const uint32_t jf = lobit(ec);
+                    uint32_t cnt;
+                    if ((C >> off) & 1u) {
+                        cnt = jf + 1u;
+                    } else {
+                        const uint32_t cer = (cexc >> (16 * c)) & 0xffffu;
+                        const uint32_t lcp = cer ? rb[c] + cer : ccarry[c];  // last chunk start + 1
+                        cnt = g * Ls[c] + jf + 2u - lcp;
                     }
+                    const uint32_t val = c ? (perm(T[1], T[0], fsA) | perm(T[3], T[2], fsB)) : (T[0] & 0xffu);
+                    *reinterpret_cast<uint16_t *>(smem + base[c]) = (uint16_t)((cnt & 0xffu) | (val << 8));
                 }
-            };
-            if (((gdst[0] | gdst[1]) & 1) == 0) sweep(std::false_type{});
-            else sweep(std::true_type{});
+            }
             team_sync<1>();  // this wave's staging writes are visible to its other lanes
 #pragma unroll
             for (int c = 0; c < 2; ++c) {
@@ -806,35 +805,37 @@ __global__ __launch_bounds__(TEAM) void tdt_encode_kernel(EncodeArgs a) {
         };
 
         if (resident) {
-            for (uint32_t r = 0; r < (uint32_t)G; ++r) {
-                if (r < RW) emit(r, dres[0], cres[0], r + 1 < RW ? rdlane(cres[1], 0) : nfb);
-                rotate();
+#pragma unroll
+            for (int r = 0; r < G; ++r) {
+                if ((uint32_t)r < RW) {
+                    uint32_t nx = nfb;
+                    if (r + 1 < G && (uint32_t)(r + 1) < RW) nx = rdlane(cres[r + 1 < G ? r + 1 : r], 0);
+                    emit((uint32_t)r, dres[r], cres[r], nx);
+                }
             }
         } else {
             // chunk masks are computed one round ahead (lane 63 needs the next round's)
             uint32_t rcarry[2] = {rin[0], rin[1]};
             uint32_t edc = edc0;
-            auto chunk_of = [&](uint32_t r, const uint4 &d) __attribute__((always_inline)) -> uint32_t {
+            auto chunk_of = [&](uint32_t r, const uint4 &d, uint4 &Tw) __attribute__((always_inline)) -> uint32_t {
                 const uint32_t g = gw0 + r * 64 + lane;
                 const uint32_t V = full_round(r) ? 0xffffu : vmask(vbytes(g));
                 uint32_t T[4];
                 tmat(d, T);
+                Tw = make_uint4(T[0], T[1], T[2], T[3]);
                 const uint32_t ed = edges(d);
                 const uint32_t m = run_mask(T, ed, edc, g, V);
                 edc = rdlane(ed, 63);
                 return chunk_round(r, m, rcarry, g, V);
             };
-            uint4 dc = load_group(gw0 + lane);
-            uint32_t Cc = chunk_of(0, dc);
+            uint4 Tc;
+            uint32_t Cc = chunk_of(0, load_group(gw0 + lane), Tc);
             for (uint32_t r = 0; r < RW; ++r) {
-                uint4 dn = make_uint4(0, 0, 0, 0);
+                uint4 Tn = make_uint4(0, 0, 0, 0);
                 uint32_t Cn = 0;
-                if (r + 1 < RW) {
-                    dn = load_group(gw0 + (r + 1) * 64 + lane);
-                    Cn = chunk_of(r + 1, dn);
-                }
-                emit(r, dc, Cc, r + 1 < RW ? rdlane(Cn, 0) : nfb);
-                dc = dn;
+                if (r + 1 < RW) Cn = chunk_of(r + 1, load_group(gw0 + (r + 1) * 64 + lane), Tn);
+                emit(r, Tc, Cc, r + 1 < RW ? rdlane(Cn, 0) : nfb);
+                Tc = Tn;
                 Cc = Cn;
             }
         }

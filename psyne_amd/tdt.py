@@ -156,6 +156,62 @@ class TdtCodec:
                                          _ptr(out_offsets), _ptr(status), self._stream(stream)))
         return out, out_offsets, status
 
+    # ---- slotted batches (no inter-message dependency: the hot path) -------------------
+    def encode_slots(self, offsets, stream=None):
+        """Slot offsets (n+1, int64, device) = prefix sum of the encode bounds."""
+        import torch
+        n = offsets.numel() - 1
+        slots = torch.empty(n + 1, dtype=torch.int64, device=offsets.device)
+        check(self._lib.tdt_encode_slots(self._h, _ptr(offsets), n, _ptr(slots), self._stream(stream)))
+        return slots
+
+    def decode_slots(self, blobs, offsets, lengths=None, status=None, stream=None):
+        """Slot offsets (n+1) = prefix sum of the decoded sizes (header parse).  With
+        `lengths`, blob i is blobs[offsets[i]:offsets[i]+lengths[i]] (offsets may then have n
+        or n+1 entries)."""
+        import torch
+        n = lengths.numel() if lengths is not None else offsets.numel() - 1
+        slots = torch.empty(n + 1, dtype=torch.int64, device=offsets.device)
+        if status is None:
+            status = torch.empty(max(n, 1), dtype=torch.int32, device=offsets.device)
+        check(self._lib.tdt_decode_slots(self._h, _ptr(blobs), _ptr(offsets), _ptr(lengths), n, _ptr(slots),
+                                         _ptr(status), self._stream(stream)))
+        return slots
+
+    def encode_into(self, data, offsets, slots=None, out=None, lengths=None, status=None, stream=None):
+        """Encode message i into out[slots[i]:slots[i+1]]; returns (out, slots, lengths, status)."""
+        import torch
+        n = offsets.numel() - 1
+        if slots is None:
+            slots = self.encode_slots(offsets, stream=stream)
+        if out is None:
+            out = torch.empty(max(int(slots[-1].item()), 1), dtype=torch.uint8, device=data.device)
+        if lengths is None:
+            lengths = torch.empty(max(n, 1), dtype=torch.int64, device=data.device)
+        if status is None:
+            status = torch.empty(max(n, 1), dtype=torch.int32, device=data.device)
+        check(self._lib.tdt_encode_batch_into(self._h, _ptr(data), _ptr(offsets), n, _ptr(out), _ptr(slots),
+                                              _ptr(lengths), _ptr(status), self._stream(stream)))
+        return out, slots, lengths, status
+
+    def decode_into(self, blobs, offsets, in_lengths=None, slots=None, out=None, lengths=None, status=None,
+                    stream=None):
+        """Decode blob i (blobs[offsets[i]:offsets[i]+in_lengths[i]], or up to offsets[i+1]) into
+        out[slots[i]:slots[i+1]]; returns (out, slots, lengths, status)."""
+        import torch
+        n = in_lengths.numel() if in_lengths is not None else offsets.numel() - 1
+        if slots is None:
+            slots = self.decode_slots(blobs, offsets, lengths=in_lengths, stream=stream)
+        if out is None:
+            out = torch.empty(max(int(slots[-1].item()), 1), dtype=torch.uint8, device=blobs.device)
+        if lengths is None:
+            lengths = torch.empty(max(n, 1), dtype=torch.int64, device=blobs.device)
+        if status is None:
+            status = torch.empty(max(n, 1), dtype=torch.int32, device=blobs.device)
+        check(self._lib.tdt_decode_batch_into(self._h, _ptr(blobs), _ptr(offsets), _ptr(in_lengths), n, _ptr(out),
+                                              _ptr(slots), _ptr(lengths), _ptr(status), self._stream(stream)))
+        return out, slots, lengths, status
+
     def decoded_sizes(self, blobs, offsets, stream=None):
         import torch
         n = offsets.numel() - 1

@@ -52,6 +52,31 @@ __global__ __launch_bounds__(256) void selftest_kernel(const uint32_t *in, uint3
     }
 }
 
+// Unaligned LDS stores/loads (ds_write_b16 at odd byte addresses, ds_read_b128 at 4-aligned
+// ones): out[l] = the u32 read back at byte 4l of a buffer where lane l wrote u16 (0x100+l) at
+// byte 2l+1, and out[64 + l] = the xor of the 4 dwords of a 16-byte read at byte 4l.
+__global__ __launch_bounds__(64) void unaligned_lds_kernel(uint32_t *out) {
+    __shared__ __attribute__((aligned(16))) uint8_t buf[512];
+    const int l = threadIdx.x;
+    for (int i = l; i < 512; i += 64) buf[i] = 0;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    uint8_t *pb = buf;
+    *reinterpret_cast<uint16_t *>(pb + 2 * l + 1) = (uint16_t)(0x100 + l);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    out[l] = *reinterpret_cast<const uint32_t *>(buf + 4 * l);
+    const uint4 q = *reinterpret_cast<const uint4 *>(pb + 4 * l);
+    out[64 + l] = q.x ^ q.y ^ q.z ^ q.w;
+}
+
+extern "C" int selftest_unaligned_lds(uint32_t *d_out) {
+    hipLaunchKernelGGL(unaligned_lds_kernel, dim3(1), dim3(64), 0, 0, d_out);
+    return hipDeviceSynchronize() == hipSuccess ? 0 : 1;
+}
+
 extern "C" int selftest_run(const uint32_t *d_in, uint32_t *d_out) {
     hipLaunchKernelGGL(selftest_kernel, dim3(1), dim3(256), 0, 0, d_in, d_out);
     return hipDeviceSynchronize() == hipSuccess ? 0 : 1;

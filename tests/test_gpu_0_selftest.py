@@ -70,3 +70,22 @@ def test_primitives():
         v = 0 if sh == 32 else int(x[l]) >> sh
         want = 0xFFFFFFFF if v == 0 else 32 - v.bit_length()
         assert o[1539 + l] == want, ("ffbh", l, v)
+
+
+def test_unaligned_lds():
+    """ds_write_b16 at odd LDS addresses (the encode staging window is congruent mod 16 with
+    an arbitrary output offset) and 16-byte LDS reads at 4-byte-aligned addresses."""
+    lib = C.CDLL(str(LIB))
+    d_out = torch.zeros(128, dtype=torch.int32, device="cuda")
+    assert lib.selftest_unaligned_lds(C.c_void_p(d_out.data_ptr())) == 0
+    o = d_out.cpu().numpy().view(np.uint32)
+    buf = bytearray(512)
+    for l in range(64):
+        v = 0x100 + l
+        buf[2 * l + 1] = v & 0xFF
+        buf[2 * l + 2] = v >> 8
+    want = np.frombuffer(bytes(buf[:256]), np.uint32)
+    assert np.array_equal(o[:64], want), "unaligned ds_write_b16"
+    words = np.frombuffer(bytes(buf), np.uint32)
+    x = np.array([words[l] ^ words[l + 1] ^ words[l + 2] ^ words[l + 3] for l in range(64)], np.uint32)
+    assert np.array_equal(o[64:128], x), "ds_read_b128 at 4-byte alignment"

@@ -351,3 +351,57 @@ def test_cpp_protocol_dropin():
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "cpp protocol OK" in r.stdout
+
+
+# ------------------------------------------------------------------ slotted batches
+def test_slotted_golden_and_roundtrip(golden):
+    """tdt_encode_batch_into / tdt_decode_batch_into: every golden encode case in its own
+    slot, byte-identical blobs, lengths, decode back through the slots."""
+    for hint in (1024, 65536):
+        for (ws, bw, cpu, mt), cases in _encode_groups(golden, "encode").items():
+            codec = make_codec(ws, mt, bw, cpu, hint)
+            buf, off = pack([c.input for c in cases])
+            d, o = torch.from_numpy(buf).cuda(), torch.from_numpy(off).cuda()
+            out, slots, lens, st = codec.encode_into(d, o)
+            torch.cuda.synchronize()
+            sl, ln, e = slots.cpu().numpy(), lens.cpu().numpy(), out.cpu().numpy()
+            sizes = np.diff(off)
+            bounds = np.array([codec.encode_bound(int(s)) for s in sizes])
+            assert np.array_equal(np.diff(sl), bounds)
+            for i, c in enumerate(cases):
+                assert int(st[i]) == 0, c.name
+                assert ln[i] == c.expected.size, c.name
+                assert e[sl[i]:sl[i] + ln[i]].tobytes() == c.expected.tobytes(), c.name
+            back, dsl, dln, dst = codec.decode_into(out, slots, in_lengths=lens)
+            torch.cuda.synchronize()
+            assert np.array_equal(dsl.cpu().numpy(), off - off[0])
+            assert int(dst[: len(cases)].abs().sum()) == 0
+            assert np.array_equal(dln.cpu().numpy()[: len(cases)], sizes)
+            assert np.array_equal(back.cpu().numpy()[: int(sizes.sum())], buf[off[0]:off[-1]])
+
+
+def test_slotted_capacity_and_errors():
+    rng = np.random.default_rng(31)
+    msgs = [rng.integers(0, 256, 4096, dtype=np.uint8) for _ in range(8)]
+    codec = make_codec()
+    buf, off = pack(msgs)
+    d, o = torch.from_numpy(buf).cuda(), torch.from_numpy(off).cuda()
+    slots = codec.encode_slots(o)
+    s = slots.cpu().numpy().copy()
+    s[4] = s[3] + 100  # slot 3 too small
+    sl = torch.from_numpy(s).cuda()
+    out = torch.empty(int(s[-1]), dtype=torch.uint8, device="cuda")
+    out, _, lens, st = codec.encode_into(d, o, slots=sl, out=out)
+    torch.cuda.synchronize()
+    st, ln = st.cpu().numpy(), lens.cpu().numpy()
+    assert st[3] == E_CAPACITY and ln[3] == 0
+    assert all(st[i] == 0 for i in range(8) if i != 3)
+    # decode side: a blob with a bad magic reports status 2 and length 0; slots skip it
+    blobs = [b"PCNU" + bytes(range(10)), b"XXXXabc", b"PCNU"]
+    bb, bo = pack(blobs)
+    dd, do = torch.from_numpy(bb).cuda(), torch.from_numpy(bo).cuda()
+    back, dsl, dln, dst = codec.decode_into(dd, do)
+    torch.cuda.synchronize()
+    assert list(dst.cpu().numpy()[:3]) == [0, 2, 0]
+    assert list(dln.cpu().numpy()[:3]) == [10, 0, 0]
+    assert back.cpu().numpy()[:10].tobytes() == bytes(range(10))

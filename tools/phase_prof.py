@@ -43,11 +43,11 @@ def run(msgs, msg_bytes, seed):
     off = torch.arange(msgs + 1, dtype=torch.int64, device=dev) * msg_bytes
     buf = (C.c_uint64 * 32)()
     for it in range(3):
-        enc, eoff, st = codec.encode_batch(data, off)
+        enc, slots, lens, st = codec.encode_into(data, off)
         torch.cuda.synchronize()
         lib.tdt_prof_read(buf)
         e = list(buf)
-        back, boff, st2 = codec.decode_batch(enc, eoff)
+        back, bslots, blens, st2 = codec.decode_into(enc, slots, in_lengths=lens)
         torch.cuda.synchronize()
         lib.tdt_prof_read(buf)
         d = list(buf)
@@ -55,10 +55,12 @@ def run(msgs, msg_bytes, seed):
     print(f"encode: {te:.4g} wave-cycles over {msgs} msgs")
     for i, name in enumerate(ENC):
         print(f"  {name:24s} {e[i] / te:6.1%}  {e[i] / msgs:12.0f} cyc/msg (sum over waves)")
+    print(f"  look-back: {e[18]} calls, {e[19]} waited, {e[16]} spins, {e[17]} windows summed")
     td = sum(d[8:12])
     print(f"decode: {td:.4g} wave-cycles")
     for i, name in DEC.items():
         print(f"  {name:24s} {d[i] / td:6.1%}  {d[i] / msgs:12.0f} cyc/msg")
+    print(f"  look-back: {d[18]} calls, {d[19]} waited, {d[16]} spins, {d[17]} windows summed")
     assert torch.equal(back, data), "round trip mismatch"
 
 
