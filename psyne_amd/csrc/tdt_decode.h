@@ -1,4 +1,4 @@
-// tdt_decode.h — batched TDT decode for CDNA4 (gfx950).
+// tdt_decode.h — batched TDT decode for CDNA4 (gfx950), v2: one wave per blob.
 //
 // Restates include/psyne/protocol/tdt_compression.hpp (reference):
 //   decode                  :271-304  size < 4 → error; UNCP → payload; else TDT
@@ -6,14 +6,21 @@
 //   simple_rle_decompress   :596-612  pairs while i+1 < len; count 0 emits nothing
 //   recombine_byte_streams  :614-637  zero-initialised output; short streams leave zeros
 //
-// Work decomposition: one TEAM-thread workgroup per blob.  Output is
-// produced in WINDOWS of TEAM 16-byte groups (thread t owns group t of the window, so
-// stores are one coalesced 16 B/lane sweep).  For every stream the window covers a range
-// [P0, P1) of stream positions.  Rounds of pairs (8 per lane) are prefix-summed across the
-// team; each non-empty pair writes its value at its start position into an LDS "heads"
-// array (u16, 0xFFFF = no head).  Each thread then fills its own 4·k positions forward
-// from the last head (carry-in from a team max-scan), zeroes positions past the decoded
-// stream length, and scatters the bytes into output words with v_perm_b32 selectors.
+// Work decomposition: one 64-lane wave per blob (no workgroup barrier, many
+// blobs in flight per CU).  The output is produced in WINDOWS of WR rounds; a round is 64
+// 16-byte groups (lane l ↔ group l).  Per window and referenced stream r (k_r byte positions
+// per word, so 64·WR·WPG·k_r stream positions):
+//   1. pairs, 8 per lane per pair-round, are prefix-summed (in-lane + DPP wave scan) and each
+//      writes a HEAD key ((position mod 16) + 1) << 8 | value at its start position into an
+//      LDS array (positions past the window land in a pad slot); the pairs that start in the
+//      window are consumed (a ballot finds the boundary lane, a scalar walk the exact pair);
+//   2. per round, lane l owns 16 consecutive positions of the round's concatenated stream
+//      planes: a packed u16 prefix-max (v_pk_max_u16) fills every position with the last
+//      head before it — the key's position tag makes "last" the maximum — seeded by a wave
+//      max-scan over lanes (and the stream's carry from the previous round);
+//   3. lane l gathers its group's bytes of every stream from the planes (4 dword LDS reads
+//      when stream segments are dword-sized) and scatters them into word order with
+//      v_perm_b32 selectors (recombine_byte_streams), one 16-byte store per lane.
 #pragma once
 #include "tdt_device.h"
 #include "tdt_encode.h"
@@ -33,57 +40,95 @@ struct DecodeArgs {
     uint32_t *ticket;
     uint32_t *errflags;
     const uint64_t *slot_off;  // slotted outputs (LB = 0)
-    const uint64_t *in_len;    // optional blob lengths (blob i = in[in_off[i] .. +in_len[i]))
     uint64_t *out_len;
+    const uint64_t *in_len;  // optional blob lengths (blob i = in[in_off[i] .. +in_len[i]))
 };
 
 constexpr int kMaxRef = 16;  // referenced streams <= word_size <= 16
+constexpr int kDecWR = 2;    // rounds per window
+constexpr int kHdrCache = 256;
 
-template <int TEAM>
 struct DecLayout {
-    static constexpr int W = TEAM / 64;
-    static constexpr int HEADS = TEAM * 16 * 2;  // u16 per stream position of a window
-    static constexpr int SLOTS = 2 * W * 4 * 4;
-    // misc (uint32): [0] msg [1] status [2] is_uncp [3] orig [4] ws [5] nref [6..7] base(u64)
-    //   [8..8+16) ref stream k, [24..) soff, [40..) npairs,
-    //   [56..56+128) selectors A/B per ref (8 each), [184..200) pidx, [200..216) pos, [216..232) carry
+    // heads: sum_r (WR·64·WPG·k_r + 16 pad) u16 <= WR·1024 + 16·16 entries
+    static constexpr int HEADS = (kDecWR * 1024 + 16 * kMaxRef) * 2;
+    static constexpr int PLANES = 1024 + 64;  // one round of plane bytes (+ slack)
+    static constexpr int HDR = kHdrCache + 16;
     static constexpr int MISC = 256 * 4;
     static constexpr int OFF_HEADS = 0;
-    static constexpr int OFF_SLOTS = OFF_HEADS + HEADS;
-    static constexpr int OFF_MISC = OFF_SLOTS + SLOTS;
+    static constexpr int OFF_PLANES = OFF_HEADS + HEADS;
+    static constexpr int OFF_HDR = OFF_PLANES + PLANES;
+    static constexpr int OFF_MISC = OFF_HDR + HDR;
     static constexpr int BYTES = OFF_MISC + MISC;
 };
 
-enum { D_MSG = 0, D_STATUS = 1, D_UNCP = 2, D_ORIG = 3, D_WS = 4, D_NREF = 5, D_BASE = 6,
-       D_K = 8, D_SOFF = 24, D_NP = 40, D_SEL = 56, D_PIDX = 184, D_POS = 200, D_CARRY = 216 };
+// misc (uint32 index)
+enum {
+    D_MSG = 0, D_STATUS = 1, D_UNCP = 2, D_ORIG = 3, D_WS = 4, D_NREF = 5, D_BASE = 6 /*u64*/, D_FAST = 8,
+    D_K = 16, D_SOFF = 32, D_NP = 48, D_OA = 64 /*4*/, D_OB = 68 /*4*/, D_SB = 72 /*16: S byte → (r<<8)|off*/,
+    D_PIDX = 96, D_POS = 112, D_CV = 128, D_SLEN = 144, D_HOFF = 160, D_PB = 176
+};
 
-template <int TEAM, int SIZES_ONLY, int LB>
-__global__ __launch_bounds__(TEAM) void tdt_decode_kernel(DecodeArgs a) {
-    using Lay = DecLayout<TEAM>;
-    constexpr int W = Lay::W;
+// 16 bytes at p (any alignment): aligned dword loads + v_alignbyte when the aligned span
+// ends inside [p, lim); byte-exact (zero-filled past `valid`) otherwise.
+__device__ __forceinline__ uint4 ld16_span(const uint8_t *p, int valid, const uint8_t *lim) {
+    const uintptr_t a = (uintptr_t)p;
+    const uintptr_t a0 = a & ~(uintptr_t)3;
+    if (valid >= 16 && a0 + 20 <= (uintptr_t)lim) {
+        const uint32_t *q = reinterpret_cast<const uint32_t *>(a0);
+        const uint32_t sh = (uint32_t)(a & 3);
+        const uint32_t w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3], w4 = q[4];
+        if (sh == 0) return make_uint4(w0, w1, w2, w3);
+        return make_uint4(__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
+                          __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh));
+    }
+    return ld16_any(p, valid);
+}
+
+template <int SIZES_ONLY, int LB>
+__global__ __launch_bounds__(64) void tdt_decode_kernel(DecodeArgs a) {
+    using Lay = DecLayout;
     __shared__ __attribute__((aligned(16))) uint8_t smem[Lay::BYTES];
-    uint16_t *heads = reinterpret_cast<uint16_t *>(smem + Lay::OFF_HEADS);
-    uint32_t *slots = reinterpret_cast<uint32_t *>(smem + Lay::OFF_SLOTS);
     uint32_t *misc = reinterpret_cast<uint32_t *>(smem + Lay::OFF_MISC);
-    const int tid = threadIdx.x;
+    uint8_t *hdrc = smem + Lay::OFF_HDR;
+    const int lane = lane_id();
     PSY_PROF_BEGIN();
 
-    if (tid == 0) misc[D_MSG] = atomicAdd(a.ticket, 1u);
-    team_sync<W>();
-    const uint32_t msg = __builtin_amdgcn_readfirstlane(misc[D_MSG]);
+    uint32_t msg = 0;
+    if (lane == 0) msg = atomicAdd(a.ticket, 1u);
+    msg = __builtin_amdgcn_readfirstlane(msg);
     if (msg >= a.n_msgs) return;
     const uint64_t boff = a.in_off[msg];
     const uint64_t len = a.in_len ? a.in_len[msg] : a.in_off[msg + 1] - boff;
     const uint8_t *blob = a.in + boff;
+    const uint8_t *blim = blob + len;
 
-    // ------------------------------------------------ header parse (thread 0)
-    if (tid == 0) {
+    // ------------------------------------------------ header cache: first 256 bytes in LDS
+    {
+        const uint64_t hc = len < (uint64_t)kHdrCache ? len : (uint64_t)kHdrCache;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t o = (uint32_t)lane * 4u + (uint32_t)i;
+            hdrc[o] = o < hc ? blob[o] : (uint8_t)0;
+        }
+    }
+    team_sync<1>();
+    const uint32_t hcl = len < (uint64_t)kHdrCache ? (uint32_t)len : (uint32_t)kHdrCache;
+    auto rd32 = [&](uint64_t off) -> uint32_t {
+        if (off + 4 <= hcl) {
+            if ((off & 3) == 0) return *reinterpret_cast<const uint32_t *>(hdrc + off);
+            return ld_u32_bytes(hdrc + off);
+        }
+        return ld_u32_bytes(blob + off);
+    };
+
+    // ------------------------------------------------ header parse (lane 0)
+    if (lane == 0) {
         uint32_t st = ST_OK, uncp = 0, orig = 0, ws = 0, nref = 0;
         uint64_t osize = 0;
         if (len < 4) {
             st = ST_SHORT;
         } else {
-            const uint32_t magic = ld_u32_bytes(blob);
+            const uint32_t magic = rd32(0);
             if (magic == kMagicUNCP) {
                 uncp = 1;
                 osize = len - 4;
@@ -92,10 +137,10 @@ __global__ __launch_bounds__(TEAM) void tdt_decode_kernel(DecodeArgs a) {
             } else if (len < 20) {
                 st = ST_TRUNCATED;
             } else {
-                orig = ld_u32_bytes(blob + 4);
-                const uint32_t ns = ld_u32_bytes(blob + 8);
-                ws = ld_u32_bytes(blob + 12);
-                const uint32_t msize = ld_u32_bytes(blob + 16);
+                orig = rd32(4);
+                const uint32_t ns = rd32(8);
+                ws = rd32(12);
+                const uint32_t msize = rd32(16);
                 const int32_t wsi = (int32_t)ws;
                 // deserialize :131-165 — header, mapping and stream table must fit
                 const uint64_t toff = 20 + 4ull * msize;
@@ -106,7 +151,7 @@ __global__ __launch_bounds__(TEAM) void tdt_decode_kernel(DecodeArgs a) {
                         st = ST_TRUNCATED;
                         break;
                     }
-                    const uint32_t sl = ld_u32_bytes(blob + off);
+                    const uint32_t sl = rd32(off);
                     off += 4;
                     if (off + sl > len) st = ST_TRUNCATED;
                     off += sl;
@@ -118,23 +163,23 @@ __global__ __launch_bounds__(TEAM) void tdt_decode_kernel(DecodeArgs a) {
                 if (st == ST_OK && wc > 0) {
                     if (msize < ws) st = ST_BAD_MAPPING;
                     for (uint32_t b = 0; b < ws && st == ST_OK; ++b) {
-                        const int32_t m = (int32_t)ld_u32_bytes(blob + 20 + 4 * b);
+                        const int32_t m = (int32_t)rd32(20 + 4 * b);
                         if (m < 0 || (uint32_t)m >= ns) st = ST_BAD_MAPPING;
                     }
                     if (st == ST_OK && (ws > 16 || (16 % ws) != 0)) st = ST_UNSUPPORTED;
                 }
-                uint32_t refc[kMaxRef];
                 if (st == ST_OK && wc > 0) {
-                    // distinct referenced streams, in order of first use
+                    // referenced streams in order of first use; stream table → data offsets
+                    uint32_t refc[kMaxRef];
                     for (uint32_t b = 0; b < ws; ++b) {
-                        const uint32_t m = ld_u32_bytes(blob + 20 + 4 * b);
+                        const uint32_t m = rd32(20 + 4 * b);
                         uint32_t r = 0;
                         while (r < nref && refc[r] != m) ++r;
                         if (r == nref) refc[nref++] = m;
                     }
                     off = toff;
                     for (uint32_t s = 0; s < ns; ++s) {
-                        const uint32_t sl = ld_u32_bytes(blob + off);
+                        const uint32_t sl = rd32(off);
                         off += 4;
                         for (uint32_t r = 0; r < nref; ++r)
                             if (refc[r] == s) {
@@ -143,36 +188,48 @@ __global__ __launch_bounds__(TEAM) void tdt_decode_kernel(DecodeArgs a) {
                             }
                         off += sl;
                     }
-                }
-                if (st == ST_OK) {
-                    osize = orig;
-                    // per referenced stream: k and the scatter selectors (recombine :622-633)
-                    const uint32_t WPG = (wc > 0) ? 16 / ws : 0;
+                    const uint32_t WPG = 16 / ws;
+                    uint32_t soffb = 0, hoff = 0, pb = 0;
+                    uint32_t fast = 1;
                     for (uint32_t r = 0; r < nref; ++r) {
                         uint32_t k = 0;
-                        for (uint32_t b = 0; b < ws; ++b) k += ld_u32_bytes(blob + 20 + 4 * b) == refc[r];
+                        for (uint32_t b = 0; b < ws; ++b) k += rd32(20 + 4 * b) == refc[r];
                         misc[D_K + r] = k;
-                        for (int q = 0; q < 4; ++q) {
-                            uint32_t A = 0x0c0c0c0cu, B = 0x0c0c0c0cu;
-                            for (int t = 0; t < 4; ++t) {
-                                const uint32_t i = 4 * q + t;  // output byte in group
-                                const uint32_t w = i / ws, b = i % ws;
-                                if (w >= WPG) continue;
-                                if (ld_u32_bytes(blob + 20 + 4 * b) != refc[r]) continue;
-                                uint32_t rank = 0;
-                                for (uint32_t bb = 0; bb < b; ++bb) rank += ld_u32_bytes(blob + 20 + 4 * bb) == refc[r];
-                                const uint32_t j = w * k + rank;
-                                if (j < 8) A = (A & ~(0xffu << (8 * t))) | (j << (8 * t));
-                                else B = (B & ~(0xffu << (8 * t))) | ((j - 8) << (8 * t));
-                            }
-                            misc[D_SEL + 8 * r + q] = A;
-                            misc[D_SEL + 8 * r + 4 + q] = B;
-                        }
                         misc[D_PIDX + r] = 0;
                         misc[D_POS + r] = 0;
-                        misc[D_CARRY + r] = 0x100;  // none
+                        misc[D_CV + r] = 0;
+                        misc[D_SLEN + r] = 0xffffffffu;
+                        misc[D_HOFF + r] = hoff;
+                        misc[D_PB + r] = pb;
+                        const uint32_t seg = WPG * k;  // S bytes of stream r per group
+                        for (uint32_t u = 0; u < seg; ++u) misc[D_SB + soffb + u] = (r << 8) | u;
+                        if (seg & 3u) fast = 0;
+                        soffb += seg;
+                        hoff += kDecWR * 64 * seg + 16;
+                        pb += 64 * seg;
+                    }
+                    misc[D_FAST] = fast;
+                    // recombine selectors: output byte i = word i/ws, position b = i%ws of
+                    // stream r = ref(mapping[b]), rank t among the positions mapped to it →
+                    // S byte Soff_r + (i/ws)·k_r + t
+                    for (int q = 0; q < 4; ++q) {
+                        uint32_t A = 0x0c0c0c0cu, B = 0x0c0c0c0cu;
+                        for (int t4 = 0; t4 < 4; ++t4) {
+                            const uint32_t i = 4 * q + t4, w = i / ws, b = i % ws;
+                            const uint32_t m = rd32(20 + 4 * b);
+                            uint32_t r = 0, so = 0;
+                            while (refc[r] != m) so += WPG * misc[D_K + r++];
+                            uint32_t rank = 0;
+                            for (uint32_t bb = 0; bb < b; ++bb) rank += rd32(20 + 4 * bb) == m;
+                            const uint32_t sidx = so + w * misc[D_K + r] + rank;
+                            if (sidx < 8) A = (A & ~(0xffu << (8 * t4))) | (sidx << (8 * t4));
+                            else B = (B & ~(0xffu << (8 * t4))) | ((sidx - 8) << (8 * t4));
+                        }
+                        misc[D_OA + q] = A;
+                        misc[D_OB + q] = B;
                     }
                 }
+                if (st == ST_OK) osize = orig;
             }
         }
         if (st != ST_OK) osize = 0;
@@ -181,166 +238,230 @@ __global__ __launch_bounds__(TEAM) void tdt_decode_kernel(DecodeArgs a) {
         misc[D_ORIG] = orig;
         misc[D_WS] = ws;
         misc[D_NREF] = nref;
+        *reinterpret_cast<uint64_t *>(misc + D_BASE) = osize;
         if constexpr (SIZES_ONLY) {
             a.sizes_out[msg] = osize;
             if (a.status) a.status[msg] = (int32_t)st;
-        } else {
-            *reinterpret_cast<uint64_t *>(misc + D_BASE) = osize;
         }
     }
     if constexpr (SIZES_ONLY) return;
-    team_sync<W>();
-    if (tid < 64) {  // wave 0: output placement (look-back on the decoded size, or slot)
-        const uint64_t osize = *reinterpret_cast<const uint64_t *>(misc + D_BASE);
-        uint64_t b;
-        bool fits;
-        if constexpr (LB) {
-            b = lookback_excl_wave(a.lookback, msg, osize, a.errflags);
-            fits = b + osize <= a.out_cap;
-        } else {
-            b = a.slot_off[msg];
-            fits = osize <= a.slot_off[msg + 1] - b;
-        }
-        if (tid == 0) {
-            uint32_t st = misc[D_STATUS];
-            *reinterpret_cast<uint64_t *>(misc + D_BASE) = b;
-            if constexpr (LB) {
-                a.out_off[msg] = b;
-                if (msg == a.n_msgs - 1) a.out_off[a.n_msgs] = b + osize;
-            }
-            if (st == ST_OK && !fits) {
-                st = ST_CAPACITY;
-                misc[D_STATUS] = st;
-            }
-            if constexpr (!LB) {
-                if (a.out_len) a.out_len[msg] = st == ST_OK ? osize : 0;
-            }
-            if (a.status) a.status[msg] = (int32_t)st;
-        }
+    team_sync<1>();
+    uint32_t st = __builtin_amdgcn_readfirstlane(misc[D_STATUS]);
+    const uint64_t osize = *reinterpret_cast<const uint64_t *>(misc + D_BASE);
+    // ------------------------------------------------ output placement
+    uint64_t ob;
+    bool fits;
+    if constexpr (LB) {
+        ob = lookback_excl_wave(a.lookback, msg, osize, a.errflags);
+        fits = ob + osize <= a.out_cap;
+    } else {
+        ob = a.slot_off[msg];
+        fits = osize <= a.slot_off[msg + 1] - ob;
     }
-    team_sync<W>();
-    const uint32_t st = __builtin_amdgcn_readfirstlane(misc[D_STATUS]);
+    if (st == ST_OK && !fits) st = ST_CAPACITY;
+    if (lane == 0) {
+        if constexpr (LB) {
+            a.out_off[msg] = ob;
+            if (msg == a.n_msgs - 1) a.out_off[a.n_msgs] = ob + osize;
+        } else {
+            if (a.out_len) a.out_len[msg] = st == ST_OK ? osize : 0;
+        }
+        if (a.status) a.status[msg] = (int32_t)st;
+    }
     if (st != ST_OK) return;
     PSY_PROF_MARK(8);
-    const uint64_t ob = *reinterpret_cast<const uint64_t *>(misc + D_BASE);
     uint8_t *dst = a.out + ob;
     if (misc[D_UNCP]) {
-        team_copy_g2g<TEAM>(dst, blob + 4, len - 4);
+        team_copy_g2g<64>(dst, blob + 4, len - 4);
         return;
     }
     const uint32_t orig = __builtin_amdgcn_readfirstlane(misc[D_ORIG]);
-    const int32_t wsi = (int32_t)__builtin_amdgcn_readfirstlane(misc[D_WS]);
-    const uint64_t wc = wsi > 0 ? orig / (uint64_t)wsi : 0;
-    const uint64_t wbytes = wc * (uint64_t)(wsi > 0 ? wsi : 0);
+    const uint32_t ws = __builtin_amdgcn_readfirstlane(misc[D_WS]);
+    const uint64_t wc = orig / ws;
+    const uint64_t wbytes = wc * ws;
     // recombine :617 zero-initialises; bytes past the last whole word stay zero
-    if (orig > wbytes) team_zero<TEAM>(dst + wbytes, orig - wbytes);
+    if (orig > wbytes) team_zero<64>(dst + wbytes, orig - wbytes);
     if (wc == 0) return;
-    const uint32_t ws = (uint32_t)wsi;
     const uint32_t WPG = 16 / ws;
     const uint32_t nref = __builtin_amdgcn_readfirstlane(misc[D_NREF]);
+    const bool fast = misc[D_FAST] != 0;
     const uint32_t ngroups = (uint32_t)((wbytes + 15) / 16);
-    const uint64_t total_pos_words = wc;
+    uint32_t OA[4], OB[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        OA[q] = __builtin_amdgcn_readfirstlane(misc[D_OA + q]);
+        OB[q] = __builtin_amdgcn_readfirstlane(misc[D_OB + q]);
+    }
+    uint16_t *heads = reinterpret_cast<uint16_t *>(smem + Lay::OFF_HEADS);
+    uint8_t *planes = smem + Lay::OFF_PLANES;
 
-    for (uint32_t gw0 = 0; gw0 < ngroups; gw0 += TEAM) {
-        const uint32_t g = gw0 + tid;
-        const int64_t vb64 = (int64_t)wbytes - 16 * (int64_t)g;
-        const uint32_t vb = vb64 >= 16 ? 16u : (vb64 <= 0 ? 0u : (uint32_t)vb64);
-        const uint32_t nvw = vb / ws;
-        uint32_t od[4] = {0, 0, 0, 0};
-        const uint64_t wend = (uint64_t)(gw0 + TEAM) * WPG < total_pos_words ? (uint64_t)(gw0 + TEAM) * WPG
-                                                                              : total_pos_words;
+    // fill lane → (stream, first plane position of the lane within the stream's round plane)
+    uint32_t fr = 0, fu = 0, fk = 0;
+    for (uint32_t r = 0; r < nref; ++r) {
+        const uint32_t pb = misc[D_PB + r], seg = 64 * WPG * misc[D_K + r];
+        if ((uint32_t)lane * 16u >= pb && (uint32_t)lane * 16u < pb + seg) {
+            fr = r;
+            fu = (uint32_t)lane * 16u - pb;
+            fk = misc[D_K + r];
+        }
+    }
+    const uint32_t f_hoff = misc[D_HOFF + fr], f_lb = misc[D_PB + fr] / 16u;
+    // recombine fast path: S dword d = 4 bytes of one stream r at plane byte pb_r + l·4k_r + x
+    uint32_t sd_pb[4] = {0, 0, 0, 0}, sd_mul[4] = {0, 0, 0, 0};
+    if (fast) {
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            const uint32_t e = __builtin_amdgcn_readfirstlane(misc[D_SB + 4 * d]);
+            const uint32_t r = e >> 8;
+            sd_pb[d] = __builtin_amdgcn_readfirstlane(misc[D_PB + r]) + (e & 0xffu);
+            sd_mul[d] = WPG * __builtin_amdgcn_readfirstlane(misc[D_K + r]);
+        }
+    }
+
+    for (uint32_t gwin = 0; gwin < ngroups; gwin += 64 * kDecWR) {
+        // ---- zero the heads of this window (16 B per lane per step)
+        for (uint32_t i = (uint32_t)lane; i < (uint32_t)Lay::HEADS / 16; i += 64)
+            reinterpret_cast<uint4 *>(heads)[i] = make_uint4(0, 0, 0, 0);
+        team_sync<1>();
+        // ---- pairs → heads, per referenced stream
         for (uint32_t r = 0; r < nref; ++r) {
             const uint32_t k = __builtin_amdgcn_readfirstlane(misc[D_K + r]);
-            const uint32_t soff = __builtin_amdgcn_readfirstlane(misc[D_SOFF + r]);
             const uint32_t np = __builtin_amdgcn_readfirstlane(misc[D_NP + r]);
-            const uint64_t P0 = (uint64_t)gw0 * WPG * k;
-            const uint64_t P1 = wend * k;
-            const uint32_t span = (uint32_t)(P1 - P0);
-            for (uint32_t i = tid; i < span; i += TEAM) heads[i] = 0xffffu;
+            const uint32_t soff = __builtin_amdgcn_readfirstlane(misc[D_SOFF + r]);
+            const uint32_t hoff = __builtin_amdgcn_readfirstlane(misc[D_HOFF + r]);
             uint32_t pidx = __builtin_amdgcn_readfirstlane(misc[D_PIDX + r]);
-            uint64_t pos = __builtin_amdgcn_readfirstlane(misc[D_POS + r]);
-            const uint32_t wcarry = __builtin_amdgcn_readfirstlane(misc[D_CARRY + r]);
-            uint32_t carry = wcarry;
-            team_sync<W>();
-            // ---- pair rounds: heads for every pair starting in [P0, P1)
-            while (pos < P1 && pidx < np) {
-                const uint32_t p0 = pidx + 8u * tid;
-                const int64_t vbytes = 2 * ((int64_t)np - (int64_t)p0);
-                const int valid = vbytes >= 16 ? 16 : (vbytes <= 0 ? 0 : (int)vbytes);
-                const uint4 pv = valid > 0 ? ld16_any(blob + soff + 2ull * p0, valid) : make_uint4(0, 0, 0, 0);
+            uint32_t pos = __builtin_amdgcn_readfirstlane(misc[D_POS + r]);
+            const uint32_t wstart = gwin * WPG * k;
+            const uint32_t wlen = kDecWR * 64 * WPG * k;
+            const uint32_t hb = Lay::OFF_HEADS + 2u * hoff;
+            while (pidx < np && pos - wstart < wlen) {
+                const uint32_t p0 = pidx + 8u * (uint32_t)lane;
+                const uint32_t nv = p0 < np ? (np - p0 < 8u ? np - p0 : 8u) : 0u;
+                const uint4 pv = nv ? ld16_span(blob + soff + 2ull * p0, (int)(2 * nv), blim) : make_uint4(0, 0, 0, 0);
                 const uint32_t pw[4] = {pv.x, pv.y, pv.z, pv.w};
-                uint32_t cnt[8], val[8], tot = 0;
+                // lane total of counts (packed u16 sums of the even bytes)
+                const uint32_t s2 = (pw[0] & 0x00ff00ffu) + (pw[1] & 0x00ff00ffu) + (pw[2] & 0x00ff00ffu) +
+                                    (pw[3] & 0x00ff00ffu);
+                const uint32_t tot = (s2 & 0xffffu) + (s2 >> 16);
+                const uint32_t linc = wave_incl_scan<OpAdd>(tot);
+                const uint32_t relb = pos - wstart + (linc - tot);  // start of this lane's first pair
+                // zero counts (never made by the encoder) and the stream's last pair-round take
+                // the predicated path
+                const bool exact = (pidx + 512u > np) || __any((pw[0] & 0xffu) == 0 || (pw[0] & 0xff0000u) == 0 ||
+                                                             (pw[1] & 0xffu) == 0 || (pw[1] & 0xff0000u) == 0 ||
+                                                             (pw[2] & 0xffu) == 0 || (pw[2] & 0xff0000u) == 0 ||
+                                                             (pw[3] & 0xffu) == 0 || (pw[3] & 0xff0000u) == 0);
+                uint32_t run = relb;
 #pragma unroll
                 for (int i = 0; i < 8; ++i) {
-                    const bool ok = 2 * i + 1 < valid;  // pairs need i+1 < len (:600-601)
-                    cnt[i] = ok ? (pw[i >> 1] >> (16 * (i & 1))) & 0xffu : 0u;
-                    val[i] = (pw[i >> 1] >> (16 * (i & 1) + 8)) & 0xffu;
-                    tot += cnt[i];
+                    const uint32_t c = (pw[i >> 1] >> (16 * (i & 1))) & 0xffu;
+                    const uint32_t v = (pw[i >> 1] >> (16 * (i & 1) + 8)) & 0xffu;
+                    const uint32_t key = (((run & 15u) << 8) + 0x100u) | v;
+                    const uint32_t slot = run < wlen ? run : wlen;  // wlen = the pad slot
+                    if (!exact || (c != 0 && (uint32_t)i < nv))
+                        *reinterpret_cast<uint16_t *>(smem + hb + 2u * slot) = (uint16_t)key;
+                    run += c;
                 }
-                uint32_t ex[1] = {tot}, tt[1];
-                team_excl_scan<W, 1, OpAdd>(ex, tt, slots);
-                uint64_t s = pos + ex[0];
-                uint32_t kc = 0, kv = 0, ke = 0;
+                // consumed = the pairs starting inside the window: every lane whose first pair
+                // starts inside is consumed up to the next lane; the last such lane is walked.
+                const uint64_t bl = __ballot(nv > 0 && relb < wlen);
+                if (bl == 0) break;  // (cannot happen: pos < window end)
+                const int L = 63 - __builtin_clzll(bl);
+                const uint32_t rbL = rdlane(relb, L), nvL = rdlane(nv, L);
+                uint32_t cw[4];
 #pragma unroll
-                for (int i = 0; i < 8; ++i) {
-                    const bool real = 2 * i + 1 < valid;
-                    if (real && s < P1) {
-                        const uint32_t li = 8u * tid + i + 1;  // local index + 1
-                        kc = li;
-                        const uint64_t e = s + cnt[i];
-                        ke = e > 0xffffffffull ? 0xffffffffu : (uint32_t)e;
-                        if (cnt[i]) {
-                            kv = (li << 8) | val[i];
-                            if (s >= P0) heads[s - P0] = (uint16_t)val[i];
-                        }
-                    }
-                    s += cnt[i];
+                for (int q = 0; q < 4; ++q) cw[q] = rdlane(pw[q], L);
+                uint32_t cons = 0, rr = rbL;
+                for (uint32_t i = 0; i < nvL; ++i) {
+                    if (rr >= wlen) break;
+                    rr += (cw[i >> 1] >> (16 * (i & 1))) & 0xffu;
+                    ++cons;
                 }
-                uint32_t mx[3] = {kc, kv, ke}, mt[3];
-                team_excl_scan<W, 3, OpMax>(mx, mt, slots + W * 4);
-                const uint32_t consumed = mt[0];
-                if (mt[1]) carry = mt[1] & 0xffu;
-                if (consumed) pos = mt[2];
-                pidx += consumed;
-                if (consumed == 0) break;  // defensive: nothing starts below P1
+                pidx += 8u * (uint32_t)L + cons;
+                pos = wstart + rr;
+                if (cons < 8u || L < 63) break;  // the window ends inside this pair-round
             }
-            PSY_PROF_MARK(9);
-            const uint64_t cover = pos < P1 ? pos : P1;
-            if (tid == 0) {
+            if (lane == 0) {
                 misc[D_PIDX + r] = pidx;
-                misc[D_POS + r] = (uint32_t)pos;
-                misc[D_CARRY + r] = carry;
+                misc[D_POS + r] = pos;
+                if (pidx >= np) misc[D_SLEN + r] = pos;  // stream exhausted: decoded length
             }
-            team_sync<W>();
-            // ---- fill forward inside this thread's group
-            const uint32_t L = nvw * k;
-            const uint64_t gpos = (uint64_t)g * WPG * k;
-            uint32_t hv[16];
-            uint32_t lastkey = 0;
-#pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                hv[j] = ((uint32_t)j < L) ? heads[gpos - P0 + j] : 0xffffu;
-                if (hv[j] != 0xffffu) lastkey = ((uint32_t)(tid + 1) << 8) | hv[j];
-            }
-            uint32_t lk[1] = {lastkey}, lt[1];
-            team_excl_scan<W, 1, OpMax>(lk, lt, slots);
-            uint32_t cur = lk[0] ? (lk[0] & 0xffu) : (wcarry & 0xffu);
-            uint32_t sb[4] = {0, 0, 0, 0};
-#pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                if (hv[j] != 0xffffu) cur = hv[j];
-                const uint32_t b = ((uint32_t)j < L && gpos + j < cover) ? cur : 0u;
-                sb[j >> 2] |= b << (8 * (j & 3));
-            }
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                od[q] |= __builtin_amdgcn_perm(sb[1], sb[0], misc[D_SEL + 8 * r + q]) |
-                         __builtin_amdgcn_perm(sb[3], sb[2], misc[D_SEL + 8 * r + 4 + q]);
-            team_sync<W>();  // heads are rewritten by the next stream
-            PSY_PROF_MARK(10);
         }
-        if (vb) st16_any(dst + 16ull * g, make_uint4(od[0], od[1], od[2], od[3]), (int)vb);
-        PSY_PROF_MARK(11);
+        team_sync<1>();
+        PSY_PROF_MARK(9);
+        // ---- per round: fill the planes, recombine, store
+        for (uint32_t rl = 0; rl < (uint32_t)kDecWR; ++rl) {
+            const uint32_t g0 = gwin + rl * 64;
+            if (g0 >= ngroups) break;
+            // lane's 16 plane positions: heads[hoff + rl·64·WPG·k + fu ..)
+            const uint32_t hidx = f_hoff + rl * 64u * WPG * fk + fu;
+            const uint4 h0 = *reinterpret_cast<const uint4 *>(heads + hidx);
+            const uint4 h1 = *reinterpret_cast<const uint4 *>(heads + hidx + 8);
+            uint32_t x[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+            // last head key of the lane (tags order the keys by position)
+            uint32_t m = pk_max_u16(pk_max_u16(pk_max_u16(x[0], x[1]), pk_max_u16(x[2], x[3])),
+                                    pk_max_u16(pk_max_u16(x[4], x[5]), pk_max_u16(x[6], x[7])));
+            m = pk_max_u16(m, m >> 16) & 0xffffu;
+            const uint32_t lk = m ? (((uint32_t)lane + 1u) << 8) | (m & 0xffu) : 0u;
+            const uint32_t ex = wave_shr1(wave_incl_scan<OpMax>(lk), 0u);
+            uint32_t seed;
+            if (ex && (ex >> 8) - 1u >= f_lb) seed = ex & 0xffu;  // a head earlier in this stream's plane
+            else seed = misc[D_CV + fr];                        // carried from the previous round
+            x[0] = pk_max_u16(x[0], seed);
+            // in-lane prefix max: within each dword, then across dwords
+#pragma unroll
+            for (int q = 0; q < 8; ++q) x[q] = pk_max_u16(x[q], x[q] << 16);
+#pragma unroll
+            for (int q = 1; q < 8; ++q) x[q] = pk_max_u16(x[q], perm(x[q - 1], x[q - 1], 0x03020302u));
+            uint4 bytes = make_uint4(perm(x[1], x[0], 0x06040200u), perm(x[3], x[2], 0x06040200u),
+                                     perm(x[5], x[4], 0x06040200u), perm(x[7], x[6], 0x06040200u));
+            // a stream that ran out of pairs leaves zeros (recombine :626-631)
+            {
+                const uint32_t slen = misc[D_SLEN + fr];
+                const uint32_t p0 = g0 * WPG * fk + fu;  // absolute position of the lane's first byte
+                if (slen != 0xffffffffu && slen < p0 + 16u) {
+                    uint32_t w[4] = {bytes.x, bytes.y, bytes.z, bytes.w};
+#pragma unroll
+                    for (int i = 0; i < 16; ++i)
+                        if (p0 + (uint32_t)i >= slen) w[i >> 2] &= ~(0xffu << (8 * (i & 3)));
+                    bytes = make_uint4(w[0], w[1], w[2], w[3]);
+                }
+            }
+            *reinterpret_cast<uint4 *>(planes + 16u * (uint32_t)lane) = bytes;
+            // carries: each stream's value at the end of its round plane
+            team_sync<1>();
+            for (uint32_t r = 0; r < nref; ++r) {
+                const uint32_t pe = misc[D_PB + r] + 64u * WPG * misc[D_K + r] - 1u;
+                if (lane == 0) misc[D_CV + r] = planes[pe];
+            }
+            // recombine: S = this group's bytes of every stream, then v_perm into word order
+            uint32_t S[4];
+            if (fast) {
+#pragma unroll
+                for (int d = 0; d < 4; ++d)
+                    S[d] = *reinterpret_cast<const uint32_t *>(planes + sd_pb[d] + (uint32_t)lane * sd_mul[d]);
+            } else {
+                S[0] = S[1] = S[2] = S[3] = 0;
+                for (int i = 0; i < 16; ++i) {
+                    const uint32_t e = misc[D_SB + i];
+                    const uint32_t r = e >> 8;
+                    if (r >= nref) break;
+                    const uint32_t seg = WPG * misc[D_K + r];
+                    S[i >> 2] |= (uint32_t)planes[misc[D_PB + r] + (uint32_t)lane * seg + (e & 0xffu)] << (8 * (i & 3));
+                }
+            }
+            const uint4 o = make_uint4(perm(S[1], S[0], OA[0]) | perm(S[3], S[2], OB[0]),
+                                       perm(S[1], S[0], OA[1]) | perm(S[3], S[2], OB[1]),
+                                       perm(S[1], S[0], OA[2]) | perm(S[3], S[2], OB[2]),
+                                       perm(S[1], S[0], OA[3]) | perm(S[3], S[2], OB[3]));
+            const uint32_t g = g0 + (uint32_t)lane;
+            if (g < ngroups) {
+                const uint64_t vb64 = wbytes - 16ull * g;
+                st16_any(dst + 16ull * g, o, vb64 >= 16 ? 16 : (int)vb64);
+            }
+            team_sync<1>();  // planes are rewritten by the next round
+        }
+        PSY_PROF_MARK(10);
     }
 }
 
