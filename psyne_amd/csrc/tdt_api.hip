@@ -186,9 +186,9 @@ int decode_common(tdt_ctx *c, bool sizes_only, const uint8_t *d_in, const uint64
     a.slot_off = d_slot_off;
     a.out_len = d_out_len;
     a.in_len = d_in_len;
-    if (sizes_only) hipLaunchKernelGGL((psy::tdt_decode_kernel<1, 1>), dim3(n_msgs), dim3(64), 0, s, a);
-    else if (slotted) hipLaunchKernelGGL((psy::tdt_decode_kernel<0, 0>), dim3(n_msgs), dim3(64), 0, s, a);
-    else hipLaunchKernelGGL((psy::tdt_decode_kernel<0, 1>), dim3(n_msgs), dim3(64), 0, s, a);
+    if (sizes_only) hipLaunchKernelGGL(psy::tdt_decode_sizes_kernel, dim3((n_msgs + 255) / 256), dim3(256), 0, s, a);
+    else if (slotted) hipLaunchKernelGGL((psy::tdt_decode_kernel<0>), dim3(n_msgs), dim3(64), 0, s, a);
+    else hipLaunchKernelGGL((psy::tdt_decode_kernel<1>), dim3(n_msgs), dim3(64), 0, s, a);
     HIPCHK(hipGetLastError());
     return TDT_OK;
 }

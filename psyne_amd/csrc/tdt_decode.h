@@ -84,7 +84,82 @@ __device__ __forceinline__ uint4 ld16_span(const uint8_t *p, int valid, const ui
     return ld16_any(p, valid);
 }
 
-template <int SIZES_ONLY, int LB>
+// Header validation of one blob: decode :271-304 (size < 4, magic), deserialize :119-170
+// (header, mapping and stream table must lie inside the blob — the reference has no bounds
+// checks there) and recombine_byte_streams :614-637's preconditions (word_size > 0, every
+// mapping entry < num_streams whenever a word exists).  rd32(off) reads the u32 at blob
+// offset off (only called for offsets proven inside the blob).  osize = the decoded size
+// (original_size, or len - 4 for UNCP), 0 on error.
+// (Written as one status chain without early returns: the hipcc 7.2 structurizer dropped the
+// success value of osize when the checks returned from inside the loops.)
+template <class RD>
+__device__ __forceinline__ uint32_t blob_check(RD &&rd32, uint64_t len, uint32_t &uncp, uint64_t &osize) {
+    uint32_t st = ST_OK, orig = 0;
+    uncp = 0;
+    if (len < 4) {
+        st = ST_SHORT;
+    } else {
+        const uint32_t magic = rd32(0);
+        if (magic == kMagicUNCP) {
+            uncp = 1;
+        } else if (magic != kMagicTDT) {
+            st = ST_MAGIC;
+        } else if (len < 20) {
+            st = ST_TRUNCATED;
+        } else {
+            orig = rd32(4);
+            const uint32_t ns = rd32(8);
+            const uint32_t ws = rd32(12);
+            const uint32_t msize = rd32(16);
+            uint64_t off = 20 + 4ull * msize;
+            if (off > len) st = ST_TRUNCATED;
+            for (uint32_t s = 0; s < ns && st == ST_OK; ++s) {
+                if (off + 4 > len) {
+                    st = ST_TRUNCATED;
+                } else {
+                    const uint32_t sl = rd32(off);
+                    off += 4;
+                    if (off + sl > len) st = ST_TRUNCATED;
+                    off += sl;
+                }
+            }
+            const int32_t wsi = (int32_t)ws;
+            if (st == ST_OK && wsi == 0) st = ST_BAD_HEADER;
+            const uint64_t wc = wsi > 0 ? orig / (uint64_t)wsi : 0;
+            if (st == ST_OK && wc > 0) {
+                if (msize < ws) st = ST_BAD_MAPPING;
+                for (uint32_t b = 0; b < ws && st == ST_OK; ++b) {
+                    const int32_t m = (int32_t)rd32(20 + 4 * b);
+                    if (m < 0 || (uint32_t)m >= ns) st = ST_BAD_MAPPING;
+                }
+                if (st == ST_OK && (ws > 16 || (16 % ws) != 0)) st = ST_UNSUPPORTED;
+            }
+        }
+    }
+    osize = st != ST_OK ? 0ull : uncp ? len - 4 : (uint64_t)orig;
+    return st;
+}
+
+// Decoded sizes (and statuses) only: one lane per blob, no LDS — the header words sit in the
+// first cache lines of each blob.
+__global__ __launch_bounds__(256) void tdt_decode_sizes_kernel(DecodeArgs a) {
+    const uint32_t msg = blockIdx.x * 256u + threadIdx.x;
+    if (msg >= a.n_msgs) return;
+    const uint64_t boff = a.in_off[msg];
+    const uint64_t len = a.in_len ? a.in_len[msg] : a.in_off[msg + 1] - boff;
+    const uint8_t *blob = a.in + boff;
+    const bool al4 = ((uintptr_t)blob & 3) == 0;
+    auto rd32 = [&](uint64_t off) -> uint32_t {
+        return (al4 && (off & 3) == 0) ? *reinterpret_cast<const uint32_t *>(blob + off) : ld_u32_bytes(blob + off);
+    };
+    uint32_t uncp;
+    uint64_t osize;
+    const uint32_t st = blob_check(rd32, len, uncp, osize);
+    a.sizes_out[msg] = osize;
+    if (a.status) a.status[msg] = (int32_t)st;
+}
+
+template <int LB>
 __global__ __launch_bounds__(64) void tdt_decode_kernel(DecodeArgs a) {
     using Lay = DecLayout;
     __shared__ __attribute__((aligned(16))) uint8_t smem[Lay::BYTES];
@@ -123,128 +198,83 @@ __global__ __launch_bounds__(64) void tdt_decode_kernel(DecodeArgs a) {
 
     // ------------------------------------------------ header parse (lane 0)
     if (lane == 0) {
-        uint32_t st = ST_OK, uncp = 0, orig = 0, ws = 0, nref = 0;
+        uint32_t uncp = 0, orig = 0, ws = 0, nref = 0;
         uint64_t osize = 0;
-        if (len < 4) {
-            st = ST_SHORT;
-        } else {
-            const uint32_t magic = rd32(0);
-            if (magic == kMagicUNCP) {
-                uncp = 1;
-                osize = len - 4;
-            } else if (magic != kMagicTDT) {
-                st = ST_MAGIC;
-            } else if (len < 20) {
-                st = ST_TRUNCATED;
-            } else {
-                orig = rd32(4);
-                const uint32_t ns = rd32(8);
-                ws = rd32(12);
-                const uint32_t msize = rd32(16);
-                const int32_t wsi = (int32_t)ws;
-                // deserialize :131-165 — header, mapping and stream table must fit
-                const uint64_t toff = 20 + 4ull * msize;
+        const uint32_t st = blob_check(rd32, len, uncp, osize);
+        if (st == ST_OK && !uncp) {
+            orig = rd32(4);
+            const uint32_t ns = rd32(8);
+            ws = rd32(12);
+            const uint64_t toff = 20 + 4ull * rd32(16);
+            if ((int32_t)ws > 0 && orig / ws > 0) {
+                // referenced streams in order of first use; stream table → data offsets
+                uint32_t refc[kMaxRef];
+                for (uint32_t b = 0; b < ws; ++b) {
+                    const uint32_t m = rd32(20 + 4 * b);
+                    uint32_t r = 0;
+                    while (r < nref && refc[r] != m) ++r;
+                    if (r == nref) refc[nref++] = m;
+                }
                 uint64_t off = toff;
-                if (off > len) st = ST_TRUNCATED;
-                for (uint32_t s = 0; s < ns && st == ST_OK; ++s) {
-                    if (off + 4 > len) {
-                        st = ST_TRUNCATED;
-                        break;
-                    }
+                for (uint32_t s = 0; s < ns; ++s) {
                     const uint32_t sl = rd32(off);
                     off += 4;
-                    if (off + sl > len) st = ST_TRUNCATED;
+                    for (uint32_t r = 0; r < nref; ++r)
+                        if (refc[r] == s) {
+                            misc[D_SOFF + r] = (uint32_t)off;
+                            misc[D_NP + r] = sl / 2;
+                        }
                     off += sl;
                 }
-                // recombine :618-631 — word_size 0 divides by zero; mapping must cover ws
-                // entries with values < num_streams whenever at least one word exists
-                const uint64_t wc = wsi > 0 ? orig / (uint64_t)wsi : 0;
-                if (st == ST_OK && wsi == 0) st = ST_BAD_HEADER;
-                if (st == ST_OK && wc > 0) {
-                    if (msize < ws) st = ST_BAD_MAPPING;
-                    for (uint32_t b = 0; b < ws && st == ST_OK; ++b) {
-                        const int32_t m = (int32_t)rd32(20 + 4 * b);
-                        if (m < 0 || (uint32_t)m >= ns) st = ST_BAD_MAPPING;
-                    }
-                    if (st == ST_OK && (ws > 16 || (16 % ws) != 0)) st = ST_UNSUPPORTED;
+                const uint32_t WPG = 16 / ws;
+                uint32_t soffb = 0, hoff = 0, pb = 0;
+                uint32_t fast = 1;
+                for (uint32_t r = 0; r < nref; ++r) {
+                    uint32_t k = 0;
+                    for (uint32_t b = 0; b < ws; ++b) k += rd32(20 + 4 * b) == refc[r];
+                    misc[D_K + r] = k;
+                    misc[D_PIDX + r] = 0;
+                    misc[D_POS + r] = 0;
+                    misc[D_CV + r] = 0;
+                    misc[D_SLEN + r] = 0xffffffffu;
+                    misc[D_HOFF + r] = hoff;
+                    misc[D_PB + r] = pb;
+                    const uint32_t seg = WPG * k;  // S bytes of stream r per group
+                    for (uint32_t u = 0; u < seg; ++u) misc[D_SB + soffb + u] = (r << 8) | u;
+                    if (seg & 3u) fast = 0;
+                    soffb += seg;
+                    hoff += kDecWR * 64 * seg + 16;
+                    pb += 64 * seg;
                 }
-                if (st == ST_OK && wc > 0) {
-                    // referenced streams in order of first use; stream table → data offsets
-                    uint32_t refc[kMaxRef];
-                    for (uint32_t b = 0; b < ws; ++b) {
+                misc[D_FAST] = fast;
+                // recombine selectors: output byte i = word i/ws, position b = i%ws of
+                // stream r = ref(mapping[b]), rank t among the positions mapped to it →
+                // S byte Soff_r + (i/ws)·k_r + t
+                for (int q = 0; q < 4; ++q) {
+                    uint32_t A = 0x0c0c0c0cu, B = 0x0c0c0c0cu;
+                    for (int t4 = 0; t4 < 4; ++t4) {
+                        const uint32_t i = 4 * q + t4, w = i / ws, b = i % ws;
                         const uint32_t m = rd32(20 + 4 * b);
-                        uint32_t r = 0;
-                        while (r < nref && refc[r] != m) ++r;
-                        if (r == nref) refc[nref++] = m;
+                        uint32_t r = 0, so = 0;
+                        while (refc[r] != m) so += WPG * misc[D_K + r++];
+                        uint32_t rank = 0;
+                        for (uint32_t bb = 0; bb < b; ++bb) rank += rd32(20 + 4 * bb) == m;
+                        const uint32_t sidx = so + w * misc[D_K + r] + rank;
+                        if (sidx < 8) A = (A & ~(0xffu << (8 * t4))) | (sidx << (8 * t4));
+                        else B = (B & ~(0xffu << (8 * t4))) | ((sidx - 8) << (8 * t4));
                     }
-                    off = toff;
-                    for (uint32_t s = 0; s < ns; ++s) {
-                        const uint32_t sl = rd32(off);
-                        off += 4;
-                        for (uint32_t r = 0; r < nref; ++r)
-                            if (refc[r] == s) {
-                                misc[D_SOFF + r] = (uint32_t)off;
-                                misc[D_NP + r] = sl / 2;
-                            }
-                        off += sl;
-                    }
-                    const uint32_t WPG = 16 / ws;
-                    uint32_t soffb = 0, hoff = 0, pb = 0;
-                    uint32_t fast = 1;
-                    for (uint32_t r = 0; r < nref; ++r) {
-                        uint32_t k = 0;
-                        for (uint32_t b = 0; b < ws; ++b) k += rd32(20 + 4 * b) == refc[r];
-                        misc[D_K + r] = k;
-                        misc[D_PIDX + r] = 0;
-                        misc[D_POS + r] = 0;
-                        misc[D_CV + r] = 0;
-                        misc[D_SLEN + r] = 0xffffffffu;
-                        misc[D_HOFF + r] = hoff;
-                        misc[D_PB + r] = pb;
-                        const uint32_t seg = WPG * k;  // S bytes of stream r per group
-                        for (uint32_t u = 0; u < seg; ++u) misc[D_SB + soffb + u] = (r << 8) | u;
-                        if (seg & 3u) fast = 0;
-                        soffb += seg;
-                        hoff += kDecWR * 64 * seg + 16;
-                        pb += 64 * seg;
-                    }
-                    misc[D_FAST] = fast;
-                    // recombine selectors: output byte i = word i/ws, position b = i%ws of
-                    // stream r = ref(mapping[b]), rank t among the positions mapped to it →
-                    // S byte Soff_r + (i/ws)·k_r + t
-                    for (int q = 0; q < 4; ++q) {
-                        uint32_t A = 0x0c0c0c0cu, B = 0x0c0c0c0cu;
-                        for (int t4 = 0; t4 < 4; ++t4) {
-                            const uint32_t i = 4 * q + t4, w = i / ws, b = i % ws;
-                            const uint32_t m = rd32(20 + 4 * b);
-                            uint32_t r = 0, so = 0;
-                            while (refc[r] != m) so += WPG * misc[D_K + r++];
-                            uint32_t rank = 0;
-                            for (uint32_t bb = 0; bb < b; ++bb) rank += rd32(20 + 4 * bb) == m;
-                            const uint32_t sidx = so + w * misc[D_K + r] + rank;
-                            if (sidx < 8) A = (A & ~(0xffu << (8 * t4))) | (sidx << (8 * t4));
-                            else B = (B & ~(0xffu << (8 * t4))) | ((sidx - 8) << (8 * t4));
-                        }
-                        misc[D_OA + q] = A;
-                        misc[D_OB + q] = B;
-                    }
+                    misc[D_OA + q] = A;
+                    misc[D_OB + q] = B;
                 }
-                if (st == ST_OK) osize = orig;
             }
         }
-        if (st != ST_OK) osize = 0;
         misc[D_STATUS] = st;
         misc[D_UNCP] = uncp;
         misc[D_ORIG] = orig;
         misc[D_WS] = ws;
         misc[D_NREF] = nref;
         *reinterpret_cast<uint64_t *>(misc + D_BASE) = osize;
-        if constexpr (SIZES_ONLY) {
-            a.sizes_out[msg] = osize;
-            if (a.status) a.status[msg] = (int32_t)st;
-        }
     }
-    if constexpr (SIZES_ONLY) return;
     team_sync<1>();
     uint32_t st = __builtin_amdgcn_readfirstlane(misc[D_STATUS]);
     const uint64_t osize = *reinterpret_cast<const uint64_t *>(misc + D_BASE);
@@ -318,6 +348,19 @@ __global__ __launch_bounds__(64) void tdt_decode_kernel(DecodeArgs a) {
         }
     }
 
+    // One pair-round (8 pairs per lane from pair index pidx) of a stream; byte-exact at the
+    // stream's end.
+    auto load_pairs = [&](uint32_t pidx_, uint32_t np_, uint32_t soff_) __attribute__((always_inline)) -> uint4 {
+        const uint32_t p0 = pidx_ + 8u * (uint32_t)lane;
+        const uint32_t nv = p0 < np_ ? (np_ - p0 < 8u ? np_ - p0 : 8u) : 0u;
+        return nv ? ld16_span(blob + soff_ + 2ull * p0, (int)(2 * nv), blim) : make_uint4(0, 0, 0, 0);
+    };
+    // The first pair-round of the next window of referenced streams 0 and 1 is loaded as soon
+    // as this window's consumption is known, so its HBM latency overlaps this window's fill,
+    // recombine and store (pf_idx = the pair index the registers hold, ~0 = none).
+    uint4 pf0 = make_uint4(0, 0, 0, 0), pf1 = make_uint4(0, 0, 0, 0);
+    uint32_t pf_idx0 = ~0u, pf_idx1 = ~0u;
+
     for (uint32_t gwin = 0; gwin < ngroups; gwin += 64 * kDecWR) {
         // ---- zero the heads of this window (16 B per lane per step)
         for (uint32_t i = (uint32_t)lane; i < (uint32_t)Lay::HEADS / 16; i += 64)
@@ -337,7 +380,10 @@ __global__ __launch_bounds__(64) void tdt_decode_kernel(DecodeArgs a) {
             while (pidx < np && pos - wstart < wlen) {
                 const uint32_t p0 = pidx + 8u * (uint32_t)lane;
                 const uint32_t nv = p0 < np ? (np - p0 < 8u ? np - p0 : 8u) : 0u;
-                const uint4 pv = nv ? ld16_span(blob + soff + 2ull * p0, (int)(2 * nv), blim) : make_uint4(0, 0, 0, 0);
+                uint4 pv;
+                if (r == 0 && pidx == pf_idx0) pv = pf0;
+                else if (r == 1 && pidx == pf_idx1) pv = pf1;
+                else pv = load_pairs(pidx, np, soff);
                 const uint32_t pw[4] = {pv.x, pv.y, pv.z, pv.w};
                 // lane total of counts (packed u16 sums of the even bytes)
                 const uint32_t s2 = (pw[0] & 0x00ff00ffu) + (pw[1] & 0x00ff00ffu) + (pw[2] & 0x00ff00ffu) +
@@ -380,6 +426,15 @@ __global__ __launch_bounds__(64) void tdt_decode_kernel(DecodeArgs a) {
                 pidx += 8u * (uint32_t)L + cons;
                 pos = wstart + rr;
                 if (cons < 8u || L < 63) break;  // the window ends inside this pair-round
+            }
+            if (pidx < np) {
+                if (r == 0) {
+                    pf0 = load_pairs(pidx, np, soff);
+                    pf_idx0 = pidx;
+                } else if (r == 1) {
+                    pf1 = load_pairs(pidx, np, soff);
+                    pf_idx1 = pidx;
+                }
             }
             if (lane == 0) {
                 misc[D_PIDX + r] = pidx;

@@ -1,0 +1,48 @@
+#!/usr/bin/env python3
+"""HBM traffic per launch from rocprofv3 --pmc passes -> profiles/<tag>_traffic.json.
+
+usage: python tools/traffic_json.py <pmc dir> <out.json> <config key>
+
+FETCH_SIZE / WRITE_SIZE are reported in KB.  MI355X_MICROARCH.md §HBM: on gfx950 FETCH_SIZE
+reports exactly half the bytes of a wide (16 B/lane) coalesced streaming read, so it is
+doubled; WRITE_SIZE reads the bytes exactly for 16-B-per-lane stores.  Per launch = mean over
+the dispatches of the kernel.
+"""
+import collections
+import csv
+import glob
+import json
+import sys
+
+
+def main():
+    root, out, key = sys.argv[1], sys.argv[2], sys.argv[3]
+    per = collections.defaultdict(lambda: collections.defaultdict(list))
+    for f in glob.glob(root + "/**/*counter_collection.csv", recursive=True):
+        for r in csv.DictReader(open(f)):
+            k = r["Kernel_Name"]
+            if "tdt_" not in k:
+                continue
+            short = k.split("(")[0].replace("void psy::", "").split("<")[0]
+            tmpl = k.split("(")[0].replace("void psy::", "")
+            per[(short, tmpl)][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    kernels = {}
+    for (short, tmpl), d in per.items():
+        if "FETCH_SIZE" not in d or "WRITE_SIZE" not in d:
+            continue
+        fetch = 2.0 * 1024 * sum(d["FETCH_SIZE"]) / len(d["FETCH_SIZE"])
+        write = 1024.0 * sum(d["WRITE_SIZE"]) / len(d["WRITE_SIZE"])
+        ent = {"template": tmpl, "fetch_bytes_corrected": fetch, "write_bytes": write,
+               "hbm_bytes_per_launch": fetch + write, "dispatches": len(d["FETCH_SIZE"])}
+        # the largest instantiation of a kernel name is the main pass (sizes-only passes are tiny)
+        if short not in kernels or ent["hbm_bytes_per_launch"] > kernels[short]["hbm_bytes_per_launch"]:
+            kernels[short] = ent
+    res = {"config": key, "kernels": kernels,
+           "method": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950 correction) and WRITE_SIZE in separate passes"}
+    with open(out, "w") as f:
+        json.dump(res, f, indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
