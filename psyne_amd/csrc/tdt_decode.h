@@ -159,6 +159,199 @@ __global__ __launch_bounds__(256) void tdt_decode_sizes_kernel(DecodeArgs a) {
     if (a.status) a.status[msg] = (int32_t)st;
 }
 
+// ---------------------------------------------------------------------------------------
+// Fast path: at most two referenced streams whose per-group segments seg_r = WPG·k_r are
+// whole dwords (every blob psyne's encoder writes for word_size 4 has this shape).
+//
+// Pair BLOCKS: a stream is read in blocks of 512 pairs (8 per lane, one 16-byte load per
+// lane); a block is prefix-summed ONCE into absolute start positions st[i] (invalid pairs —
+// count 0 or past the stream — get start ~0) and packed head keys, and stays in registers
+// across output windows until the window passes its end.  Per window and block, every pair
+// writes its key at slot min(st - wstart, wlen): pairs outside the window land in the pad
+// slot, so the write is branch-free (3 VALU + 1 ds_write_b16 per pair).
+//
+// Keys are gen << 13 | (pos mod 16 + 1) << 8 | value (a 5-bit tag) with gen = window index
+// mod 8, so the head array is only zeroed every 8 windows: stale keys compare below the
+// current window's seed key (gen << 13 | value) and below every current head.
+//
+// Fill, per round of 64 groups: lane l owns 16 consecutive positions of the round's two
+// stream planes (stream 0: lanes [0, 4·seg0), stream 1 after); an in-lane u16 prefix max,
+// seeded by a wave max-scan of each lane's last head (restricted to its own stream) or by the
+// stream's carry, gives every position its run's value.  Planes → LDS; each lane gathers its
+// group's segments (dword reads) and v_perm's them into word order (recombine :614-637).
+constexpr int kFastWR = kDecWR;
+
+__device__ __forceinline__ void decode_fast(uint32_t *misc, uint8_t *smem, const uint8_t *blob, const uint8_t *blim,
+                                            uint8_t *dst, uint32_t ngroups, uint64_t wbytes, uint32_t WPG,
+                                            uint32_t nref, const uint32_t (&OA)[4], const uint32_t (&OB)[4]) {
+    using Lay = DecLayout;
+    constexpr uint32_t WR = kFastWR;
+    const uint32_t lane = (uint32_t)lane_id();
+    uint16_t *heads = reinterpret_cast<uint16_t *>(smem + Lay::OFF_HEADS);
+    uint8_t *planes = smem + Lay::OFF_PLANES;
+    const bool two = nref == 2;
+    const uint32_t seg[2] = {WPG * (uint32_t)__builtin_amdgcn_readfirstlane(misc[D_K + 0]),
+                             two ? WPG * (uint32_t)__builtin_amdgcn_readfirstlane(misc[D_K + 1]) : 0u};
+    const uint32_t np[2] = {(uint32_t)__builtin_amdgcn_readfirstlane(misc[D_NP + 0]),
+                            two ? (uint32_t)__builtin_amdgcn_readfirstlane(misc[D_NP + 1]) : 0u};
+    const uint32_t soff[2] = {(uint32_t)__builtin_amdgcn_readfirstlane(misc[D_SOFF + 0]),
+                              two ? (uint32_t)__builtin_amdgcn_readfirstlane(misc[D_SOFF + 1]) : 0u};
+    const uint32_t wlen[2] = {WR * 64u * seg[0], WR * 64u * seg[1]};
+    const uint32_t hbase[2] = {(uint32_t)Lay::OFF_HEADS, (uint32_t)Lay::OFF_HEADS + 2u * (wlen[0] + 16u)};
+    // fill lane
+    const bool f1 = lane * 16u >= 64u * seg[0];
+    const uint32_t fu = f1 ? lane * 16u - 64u * seg[0] : lane * 16u;
+    const uint32_t fseg = f1 ? seg[1] : seg[0];
+    const uint32_t f_lb = f1 ? 4u * seg[0] : 0u;  // first lane of this lane's stream plane
+    const uint32_t fh = (f1 ? hbase[1] : hbase[0]) + 2u * fu;
+    const uint32_t last_lane0 = 4u * seg[0] - 1u;  // lane holding stream 0's last plane byte
+    // recombine: S dword d = plane bytes sd_pb[d] + lane·sd_mul[d] (4 bytes of one stream)
+    uint32_t sd_pb[4], sd_mul[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        const uint32_t e = __builtin_amdgcn_readfirstlane(misc[D_SB + 4 * d]);
+        const uint32_t r = e >> 8;
+        sd_pb[d] = (r ? 64u * seg[0] : 0u) + (e & 0xffu);
+        sd_mul[d] = r ? seg[1] : seg[0];
+    }
+
+    // per stream block state (uniform) and registers (per lane)
+    uint32_t bidx[2] = {0u, 0u};      // pair index of the NEXT block to load
+    uint32_t bend[2] = {0u, 0u};      // absolute end position of the loaded block
+    uint32_t slen[2] = {~0u, ~0u};    // decoded stream length once its last block is loaded
+    bool have[2] = {false, false};
+    uint32_t st[2][8];
+    uint32_t kp[2][4];  // packed keys without gen: key(2j) | key(2j+1) << 16
+    uint32_t cv[2] = {0u, 0u};  // carry: value of the last plane position of the previous round
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) st[r][i] = ~0u;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) kp[r][j] = 0u;
+    }
+
+    auto load_block = [&](int r) __attribute__((always_inline)) {
+        const uint32_t p0 = bidx[r] + 8u * lane;
+        const uint32_t nv = p0 < np[r] ? (np[r] - p0 < 8u ? np[r] - p0 : 8u) : 0u;
+        const uint4 pv = nv ? ld16_span(blob + soff[r] + 2ull * p0, (int)(2 * nv), blim) : make_uint4(0, 0, 0, 0);
+        const uint32_t pw[4] = {pv.x, pv.y, pv.z, pv.w};
+        const uint32_t s2 = (pw[0] & 0x00ff00ffu) + (pw[1] & 0x00ff00ffu) + (pw[2] & 0x00ff00ffu) + (pw[3] & 0x00ff00ffu);
+        const uint32_t tot = (s2 & 0xffffu) + (s2 >> 16);
+        const uint32_t linc = wave_incl_scan<OpAdd>(tot);
+        uint32_t run = bend[r] + linc - tot;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t w = pw[j];
+            const uint32_t c0 = w & 0xffu, c1 = (w >> 16) & 0xffu;
+            // key = (pos mod 16 + 1) << 8 | value; value bytes 1 and 3 of the dword
+            const uint32_t k0 = ((((run & 15u) + 1u) << 8) | ((w >> 8) & 0xffu));
+            st[r][2 * j] = (c0 != 0u && (uint32_t)(2 * j) < nv) ? run : ~0u;
+            run += c0;
+            const uint32_t k1 = ((((run & 15u) + 1u) << 8) | (w >> 24));
+            st[r][2 * j + 1] = (c1 != 0u && (uint32_t)(2 * j + 1) < nv) ? run : ~0u;
+            run += c1;
+            kp[r][j] = k0 | (k1 << 16);
+        }
+        bend[r] += rdlane(linc, 63);
+        bidx[r] += 512u;
+        have[r] = true;
+        if (bidx[r] >= np[r]) slen[r] = bend[r];
+    };
+    auto write_keys = [&](int r, uint32_t wstart, uint32_t genk) __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t k = kp[r][j] | genk;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const uint32_t rel = st[r][2 * j + h] - wstart;
+                const uint32_t slot = rel < wlen[r] ? rel : wlen[r];
+                *reinterpret_cast<uint16_t *>(smem + hbase[r] + 2u * slot) = (uint16_t)(h ? (k >> 16) : k);
+            }
+        }
+    };
+
+    uint32_t win = 0;
+    for (uint32_t gwin = 0; gwin < ngroups; gwin += 64u * WR, ++win) {
+        const uint32_t gen = win & 7u;
+        if (gen == 0) {
+            // (re)initialise the head array every 8 windows
+            for (uint32_t i = lane; i < (uint32_t)Lay::HEADS / 16; i += 64)
+                reinterpret_cast<uint4 *>(heads)[i] = make_uint4(0, 0, 0, 0);
+            team_sync<1>();
+        }
+        const uint32_t genk = (gen << 13) | (gen << 29);
+        // ---- pairs → heads
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            if (r == 1 && !two) break;
+            const uint32_t wstart = gwin * seg[r], wend = wstart + wlen[r];
+            if (have[r]) write_keys(r, wstart, genk);
+            // blocks whose first pair starts inside this window
+            while (bend[r] < wend && bidx[r] < np[r]) {
+                load_block(r);
+                write_keys(r, wstart, genk);
+            }
+        }
+        team_sync<1>();
+        // ---- per round: fill, recombine, store
+        for (uint32_t rl = 0; rl < WR; ++rl) {
+            const uint32_t g0 = gwin + rl * 64u;
+            if (g0 >= ngroups) break;
+            const uint32_t hoffb = fh + 2u * rl * 64u * fseg;
+            const uint4 h0 = *reinterpret_cast<const uint4 *>(smem + hoffb);
+            const uint4 h1 = *reinterpret_cast<const uint4 *>(smem + hoffb + 16);
+            uint32_t x[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+            uint32_t m = pk_max_u16(pk_max_u16(pk_max_u16(x[0], x[1]), pk_max_u16(x[2], x[3])),
+                                    pk_max_u16(pk_max_u16(x[4], x[5]), pk_max_u16(x[6], x[7])));
+            m = pk_max_u16(m, m >> 16) & 0xffffu;
+            // a current head exists in the lane iff the max key carries this window's gen and a tag
+            const bool hv = (m >> 13) == gen && ((m >> 8) & 31u) != 0u;
+            const uint32_t lk = hv ? ((lane + 1u) << 8) | (m & 0xffu) : 0u;
+            const uint32_t ex = wave_shr1(wave_incl_scan<OpMax>(lk), 0u);
+            const uint32_t carry = f1 ? cv[1] : cv[0];
+            const uint32_t seedv = (ex && (ex >> 8) - 1u >= f_lb) ? (ex & 0xffu) : carry;
+            const uint32_t seed = (gen << 13) | seedv;
+            x[0] = pk_max_u16(x[0], seed);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) x[q] = pk_max_u16(x[q], x[q] << 16);
+#pragma unroll
+            for (int q = 1; q < 8; ++q) x[q] = pk_max_u16(x[q], perm(x[q - 1], x[q - 1], 0x03020302u));
+            uint32_t bw[4] = {perm(x[1], x[0], 0x06040200u), perm(x[3], x[2], 0x06040200u),
+                              perm(x[5], x[4], 0x06040200u), perm(x[7], x[6], 0x06040200u)};
+            // a stream that ran out of pairs leaves zeros (recombine :626-631)
+            const uint32_t rend0 = (g0 + 64u) * seg[0], rend1 = (g0 + 64u) * seg[1];
+            if (slen[0] < rend0 || (two && slen[1] < rend1)) {
+                const uint32_t sl = f1 ? slen[1] : slen[0];
+                const uint32_t p0 = g0 * fseg + fu;
+                const uint32_t keep = sl <= p0 ? 0u : (sl - p0 >= 16u ? 16u : sl - p0);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const uint32_t kq = keep <= 4u * q ? 0u : (keep - 4u * q >= 4u ? 4u : keep - 4u * q);
+                    bw[q] &= kq >= 4u ? 0xffffffffu : ((1u << (8u * kq)) - 1u);
+                }
+            }
+            cv[0] = rdlane(bw[3], (int)last_lane0) >> 24;
+            if (two) cv[1] = rdlane(bw[3], 63) >> 24;
+            *reinterpret_cast<uint4 *>(planes + 16u * lane) = make_uint4(bw[0], bw[1], bw[2], bw[3]);
+            team_sync<1>();
+            uint32_t S[4];
+#pragma unroll
+            for (int d = 0; d < 4; ++d) S[d] = *reinterpret_cast<const uint32_t *>(planes + sd_pb[d] + lane * sd_mul[d]);
+            const uint4 o = make_uint4(perm(S[1], S[0], OA[0]) | perm(S[3], S[2], OB[0]),
+                                       perm(S[1], S[0], OA[1]) | perm(S[3], S[2], OB[1]),
+                                       perm(S[1], S[0], OA[2]) | perm(S[3], S[2], OB[2]),
+                                       perm(S[1], S[0], OA[3]) | perm(S[3], S[2], OB[3]));
+            const uint32_t g = g0 + lane;
+            if (g < ngroups) {
+                const uint64_t vb64 = wbytes - 16ull * g;
+                st16_any(dst + 16ull * g, o, vb64 >= 16 ? 16 : (int)vb64);
+            }
+            team_sync<1>();  // planes are rewritten by the next round
+        }
+    }
+}
+
 template <int LB>
 __global__ __launch_bounds__(64) void tdt_decode_kernel(DecodeArgs a) {
     using Lay = DecLayout;
@@ -325,6 +518,13 @@ __global__ __launch_bounds__(64) void tdt_decode_kernel(DecodeArgs a) {
     uint16_t *heads = reinterpret_cast<uint16_t *>(smem + Lay::OFF_HEADS);
     uint8_t *planes = smem + Lay::OFF_PLANES;
 
+    if (fast && nref <= 2) {
+        decode_fast(misc, smem, blob, blim, dst, ngroups, wbytes, WPG, nref, OA, OB);
+        return;
+    }
+
+    // ---------------------------------------------------------------- generic path
+    // (more than two referenced streams, or stream segments that are not whole dwords)
     // fill lane → (stream, first plane position of the lane within the stream's round plane)
     uint32_t fr = 0, fu = 0, fk = 0;
     for (uint32_t r = 0; r < nref; ++r) {
