@@ -43,8 +43,8 @@
 
 namespace psy {
 
-__constant__ double c_log2_tab[128] = PSY_LOG2_TAB_INIT;
-__constant__ double c_log2_tab2[128] = PSY_LOG2_TAB2_INIT;
+__constant__ __attribute__((aligned(16))) double c_log2_tab[128] = PSY_LOG2_TAB_INIT;
+__constant__ __attribute__((aligned(16))) double c_log2_tab2[128] = PSY_LOG2_TAB2_INIT;
 
 enum { MODE_ENCODE = 0, MODE_MAPPED = 1, MODE_ANALYZE = 2 };
 
@@ -91,14 +91,19 @@ struct EncLayout {
     static constexpr int WSTAGE = 2 * WREGION + 16;  // both streams + a junk pair, per wave
     static constexpr int STAGE = W * WSTAGE;
     static constexpr int TERMS = TB * 256 * 16;
-    static constexpr int UNION = STAGE > TERMS ? STAGE : TERMS;
+    // log2 tables (2 KiB) live in the union after the terms: both are dead by pass B
+    static constexpr int TERMS_LOG2 = TERMS + 2048;
+    static constexpr int UNION = STAGE > TERMS_LOG2 ? STAGE : TERMS_LOG2;
     static constexpr int SLOTS = W * 8 * 4;
     static constexpr int MISC = 512;
+    static constexpr int WM = 128;  // per-wave mapping state (uint32)
     static constexpr int OFF_HIST = 0;
     static constexpr int OFF_UNION = OFF_HIST + HIST;
+    static constexpr int OFF_LOG2 = OFF_UNION + TERMS;
     static constexpr int OFF_SLOTS = OFF_UNION + UNION;
     static constexpr int OFF_MISC = OFF_SLOTS + SLOTS;
-    static constexpr int BYTES = OFF_MISC + MISC;
+    static constexpr int OFF_WMISC = OFF_MISC + MISC;
+    static constexpr int BYTES = OFF_WMISC + WM * 4;
     static_assert((1 << LOG_HC) == HC, "histogram copies");
 };
 
@@ -147,15 +152,29 @@ __global__ __launch_bounds__(TEAM) void tdt_encode_kernel(EncodeArgs a) {
     const int wv = tid >> 6;
     PSY_PROF_BEGIN();
 
-    if (tid == 0) misc[M_MSG] = atomicAdd(a.ticket, 1u);
-    team_sync<W>();
-    const uint32_t msg = __builtin_amdgcn_readfirstlane(misc[M_MSG]);
+    // Message id: the look-back needs ids in dispatch order (atomic ticket); slotted outputs
+    // have no inter-message dependency, so the workgroup id serves.
+    uint32_t msg;
+    if constexpr (LB) {
+        if (tid == 0) misc[M_MSG] = atomicAdd(a.ticket, 1u);
+        team_sync<W>();
+        msg = __builtin_amdgcn_readfirstlane(misc[M_MSG]);
+    } else {
+        msg = blockIdx.x;
+    }
     if (msg >= a.n_msgs) return;
     PSY_PROF_MARK(0);
 
     const uint64_t off0 = a.in_off[msg];
     const uint64_t n = a.in_off[msg + 1] - off0;
     const uint8_t *base = a.in + off0;
+    // slotted outputs: the slot is known now; loading it here keeps its latency off the
+    // critical path between the count pass and the emit pass
+    uint64_t slot_b = 0, slot_e = 0;
+    if constexpr (!LB) {
+        slot_b = a.slot_off[msg];
+        slot_e = a.slot_off[msg + 1];
+    }
 
     // Output placement of an E-byte result (all threads call it): returns the offset in
     // a.out and whether the result fits.
@@ -174,8 +193,8 @@ __global__ __launch_bounds__(TEAM) void tdt_encode_kernel(EncodeArgs a) {
                 if (msg == a.n_msgs - 1) a.out_off[a.n_msgs] = ob + E;
             }
         } else {
-            ob = a.slot_off[msg];
-            fits = E <= a.slot_off[msg + 1] - ob;
+            ob = slot_b;
+            fits = E <= slot_e - ob;
             if (tid == 0 && a.out_len) a.out_len[msg] = fits ? E : 0;
         }
         return ob;
@@ -259,19 +278,21 @@ __global__ __launch_bounds__(TEAM) void tdt_encode_kernel(EncodeArgs a) {
         }
     };
 
+    // The message's mapping state: after the entropy terms wave 0 alone derives entropies,
+    // mapping, slot layout and selectors (wave-local syncs), then ONE workgroup barrier.
+    uint32_t *wm = reinterpret_cast<uint32_t *>(smem + Lay::OFF_WMISC);
+
     // ------------------------------------------------------------ mapping (analysis)
     if constexpr (MODE == MODE_MAPPED) {
-        if (tid == 0) {
-            uint32_t bad = 0;
-            for (int b = 0; b < WS; ++b) {
-                int32_t m = a.mapping_in[(uint64_t)msg * WS + b];
-                bad |= (m < 0 || m > 1);
-                misc[M_MAP + b] = (uint32_t)(m & 1);
-            }
-            misc[M_STATUS] = bad;
+        uint32_t bad = 0;
+        if (lane < WS) {
+            const int32_t m = a.mapping_in[(uint64_t)msg * WS + lane];
+            bad = (m < 0 || m > 1) ? 1u : 0u;
+            wm[M_MAP + lane] = (uint32_t)(m & 1);
         }
-        team_sync<W>();
-        if (misc[M_STATUS]) {
+        const bool anybad = __any(bad);
+        team_sync<1>();
+        if (anybad) {
             // invalid caller mapping: publish an empty output for this message
             bool fits;
             (void)place(0, fits);
@@ -285,6 +306,11 @@ __global__ __launch_bounds__(TEAM) void tdt_encode_kernel(EncodeArgs a) {
         // lanes to the same address when they hold the same nonzero value.
         uint32_t *hist = reinterpret_cast<uint32_t *>(smem + Lay::OFF_HIST);
         for (int i = tid; i < WS * Lay::PS; i += TEAM) hist[i] = 0;
+        // glibc log2 tables → LDS (the bins' log2 evaluations read them with per-lane indices)
+        for (int i = tid; i < 128; i += TEAM) {
+            const uint4 v = reinterpret_cast<const uint4 *>(i < 64 ? c_log2_tab : c_log2_tab2)[i & 63];
+            reinterpret_cast<uint4 *>(smem + Lay::OFF_LOG2)[i] = v;
+        }
         team_sync<W>();
         const uint32_t zoff = (uint32_t)lane * 4u;
         const uint32_t coff = (64u + ((uint32_t)lane & (Lay::HC - 1))) * 4u;
@@ -305,12 +331,6 @@ __global__ __launch_bounds__(TEAM) void tdt_encode_kernel(EncodeArgs a) {
         team_sync<W>();
         PSY_PROF_MARK(1);
 
-        // bin 0 = copies + the 64 per-lane zero bins
-        for (int b = wv; b < WS; b += W) {
-            const uint32_t z = wave_reduce<OpAdd>(hist[b * Lay::PS + lane]);
-            if (lane == 0) hist[b * Lay::PS + 64] += z;  // copy 0 of bin 0
-        }
-        team_sync<W>();
         auto count = [&](int b, int v) __attribute__((always_inline)) -> uint32_t {
             uint32_t c = 0;
 #pragma unroll
@@ -320,16 +340,22 @@ __global__ __launch_bounds__(TEAM) void tdt_encode_kernel(EncodeArgs a) {
 
         // entropies: calculate_entropy :470-480, TB byte positions per batch.  Each bin's
         // (-prob, log2 prob) is computed in parallel (0, 0 for an empty bin, so the chain
-        // needs no select: fma(0, 0, e) == e for the non-negative running sum); one lane per
-        // position then runs the exact fma chain in bin order.
+        // needs no select: fma(0, 0, e) == e for the non-negative running sum); then in every
+        // wave one lane per position runs the exact fma chain in bin order.
         double *terms = reinterpret_cast<double *>(smem + Lay::OFF_UNION);
+        const double *ltab = reinterpret_cast<const double *>(smem + Lay::OFF_LOG2);
         const double total = (double)wc;
         for (int q0 = 0; q0 < WS; q0 += Lay::TB) {
+            if (q0 > 0) team_sync<W>();  // every wave's chain has read the previous batch
             for (int i = tid; i < Lay::TB * 256; i += TEAM) {
-                const int b = q0 + i / 256;
+                const int b = q0 + i / 256;  // wave-uniform
                 double np = 0.0, L = 0.0;
                 if (b < WS) {
-                    const uint32_t c = count(b, i & 255);
+                    uint32_t c = count(b, i & 255);
+                    if ((i & 255) < 64) {  // wave-uniform: bin 0 adds the 64 per-lane zero bins
+                        const uint32_t z = wave_reduce<OpAdd>(hist[b * Lay::PS + lane]);
+                        if (lane == 0) c += z;
+                    }
                     if constexpr (MODE == MODE_ANALYZE) {
                         if (a.hist_out) a.hist_out[((uint64_t)msg * WS + b) * 256 + (i & 255)] = c;
                     }
@@ -338,7 +364,7 @@ __global__ __launch_bounds__(TEAM) void tdt_encode_kernel(EncodeArgs a) {
                         {
 #pragma clang fp contract(off)
                             prob = (double)c / total;
-                            L = psy_log2_glibc(prob, c_log2_tab, c_log2_tab2);
+                            L = psy_log2_glibc(prob, ltab, ltab + 128);
                         }
                         np = -prob;
                     }
@@ -347,22 +373,22 @@ __global__ __launch_bounds__(TEAM) void tdt_encode_kernel(EncodeArgs a) {
                 terms[2 * i + 1] = L;
             }
             team_sync<W>();
-            if (tid < Lay::TB && q0 + tid < WS) {
-                const int b = q0 + tid;
-                const double2 *tp = reinterpret_cast<const double2 *>(terms) + tid * 256;
+            if (wv == 0 && lane < Lay::TB && q0 + lane < WS) {
+                const int b = q0 + lane;
+                const double2 *tp = reinterpret_cast<const double2 *>(terms) + lane * 256;
                 double e = 0.0;
 #pragma unroll 16
                 for (int v = 0; v < 256; ++v) {
                     const double2 t = tp[v];
                     e = __builtin_fma(t.x, t.y, e);
                 }
-                reinterpret_cast<double *>(misc + M_ENT)[b] = e;
+                reinterpret_cast<double *>(wm + M_ENT)[b] = e;
             }
-            team_sync<W>();
         }
+        team_sync<1>();
         // perform_clustering :507-525
         if (tid == 0) {
-            const double *ent = reinterpret_cast<const double *>(misc + M_ENT);
+            const double *ent = reinterpret_cast<const double *>(wm + M_ENT);
             double sum = 0.0;
             for (int b = 0; b < WS; ++b) sum += ent[b];
             double thr;
@@ -370,14 +396,14 @@ __global__ __launch_bounds__(TEAM) void tdt_encode_kernel(EncodeArgs a) {
 #pragma clang fp contract(off)
                 thr = sum / (double)WS;
             }
-            for (int b = 0; b < WS; ++b) misc[M_MAP + b] = ent[b] > thr ? 1u : 0u;
+            for (int b = 0; b < WS; ++b) wm[M_MAP + b] = ent[b] > thr ? 1u : 0u;
         }
-        team_sync<W>();
+        team_sync<1>();
         if constexpr (MODE == MODE_ANALYZE) {
             const uint64_t mb = (uint64_t)msg * WS;
             if (tid < WS) {
-                if (a.ent_out) a.ent_out[mb + tid] = reinterpret_cast<const double *>(misc + M_ENT)[tid];
-                if (a.map_out) a.map_out[mb + tid] = (int32_t)misc[M_MAP + tid];
+                if (a.ent_out) a.ent_out[mb + tid] = reinterpret_cast<const double *>(wm + M_ENT)[tid];
+                if (a.map_out) a.map_out[mb + tid] = (int32_t)wm[M_MAP + tid];
             }
             if (tid == 0 && a.status) a.status[msg] = ST_OK;
             return;
@@ -385,69 +411,69 @@ __global__ __launch_bounds__(TEAM) void tdt_encode_kernel(EncodeArgs a) {
     }
 
     if constexpr (MODE != MODE_ANALYZE) {
-        // ------------------------------------------------ slot layout (thread 0)
+        // ------------------------------------------------ slot layout (wave 0)
         // separate_byte_streams :527-549: slot j < L0 is stream-0 byte j of the group
         // (word j / k0, position pos0[j % k0]); slot j >= L0 is stream-1 byte j - L0.
-        // 16 threads: slot j's source byte in the group (no per-thread arrays: scratch-free)
+        // 16 lanes: slot j's source byte in the group (no per-thread arrays: scratch-free)
         if (tid < 16) {
             uint32_t k[2] = {0, 0};
-            for (int b = 0; b < WS; ++b) k[misc[M_MAP + b]]++;
+            for (int b = 0; b < WS; ++b) k[wm[M_MAP + b]]++;
             const uint32_t L0 = WPG * k[0];
-            const uint32_t j = (uint32_t)tid;
+            const uint32_t j = (uint32_t)lane;
             const uint32_t c = j < L0 ? 0u : 1u;
             const uint32_t jj = c ? j - L0 : j;
             const uint32_t rank = jj % k[c];
             uint32_t b = 0, seen = 0;
             for (int bb = 0; bb < WS; ++bb) {
-                if (misc[M_MAP + bb] == c) {
+                if (wm[M_MAP + bb] == c) {
                     if (seen == rank) b = bb;
                     ++seen;
                 }
             }
-            misc[M_SB + j] = (jj / k[c]) * WS + b;
+            wm[M_SB + j] = (jj / k[c]) * WS + b;
             if (j == 0) {
-                misc[M_NS] = k[1] ? 2u : 1u;
-                misc[M_L0] = L0;
-                misc[M_K0] = k[0];
-                misc[M_K1] = k[1];
+                wm[M_NS] = k[1] ? 2u : 1u;
+                wm[M_L0] = L0;
+                wm[M_K0] = k[0];
+                wm[M_K1] = k[1];
             }
         }
-        team_sync<W>();
+        team_sync<1>();
         if (tid < 5) {
-            const uint32_t L0 = misc[M_L0];
-            const bool two = misc[M_NS] == 2;
+            const uint32_t L0 = wm[M_L0];
+            const bool two = wm[M_NS] == 2;
             uint32_t A = 0x0c0c0c0cu, B = 0x0c0c0c0cu;
             for (int t = 0; t < 4; ++t) {
                 // T[q] byte t = slot 4t + q; edges byte 0 stream-0 last slot, byte 1 slot 15,
                 // byte 2 stream-1 first slot
                 uint32_t s = 0xffu;
-                if (tid < 4) s = misc[M_SB + 4 * t + tid];
-                else if (t == 0 && L0 > 0) s = misc[M_SB + L0 - 1];
-                else if (t == 1) s = misc[M_SB + 15];
-                else if (t == 2 && two) s = misc[M_SB + L0];
+                if (lane < 4) s = wm[M_SB + 4 * t + lane];
+                else if (t == 0 && L0 > 0) s = wm[M_SB + L0 - 1];
+                else if (t == 1) s = wm[M_SB + 15];
+                else if (t == 2 && two) s = wm[M_SB + L0];
                 if (s == 0xffu) continue;
                 if (s < 8) A = (A & ~(0xffu << (8 * t))) | (s << (8 * t));
                 else B = (B & ~(0xffu << (8 * t))) | ((s - 8) << (8 * t));
             }
-            misc[tid < 4 ? M_SELA + tid : M_EDA] = A;
-            misc[tid < 4 ? M_SELB + tid : M_EDB] = B;
+            wm[lane < 4 ? M_SELA + lane : M_EDA] = A;
+            wm[lane < 4 ? M_SELB + lane : M_EDB] = B;
         }
         team_sync<W>();
-        const uint32_t ns = __builtin_amdgcn_readfirstlane(misc[M_NS]);
+        const uint32_t ns = __builtin_amdgcn_readfirstlane(wm[M_NS]);
         const bool ns2 = ns == 2;
-        const uint32_t L0 = __builtin_amdgcn_readfirstlane(misc[M_L0]);
-        const uint32_t k0 = __builtin_amdgcn_readfirstlane(misc[M_K0]);
-        const uint32_t k1 = __builtin_amdgcn_readfirstlane(misc[M_K1]);
+        const uint32_t L0 = __builtin_amdgcn_readfirstlane(wm[M_L0]);
+        const uint32_t k0 = __builtin_amdgcn_readfirstlane(wm[M_K0]);
+        const uint32_t k1 = __builtin_amdgcn_readfirstlane(wm[M_K1]);
         const uint32_t Ls[2] = {L0, ns2 ? 16u - L0 : 0u};
         const uint32_t lowL0 = L0 >= 16 ? 0xffffu : ((1u << L0) - 1u);
         uint32_t selA[4], selB[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            selA[q] = __builtin_amdgcn_readfirstlane(misc[M_SELA + q]);
-            selB[q] = __builtin_amdgcn_readfirstlane(misc[M_SELB + q]);
+            selA[q] = __builtin_amdgcn_readfirstlane(wm[M_SELA + q]);
+            selB[q] = __builtin_amdgcn_readfirstlane(wm[M_SELB + q]);
         }
-        const uint32_t edA = __builtin_amdgcn_readfirstlane(misc[M_EDA]);
-        const uint32_t edB = __builtin_amdgcn_readfirstlane(misc[M_EDB]);
+        const uint32_t edA = __builtin_amdgcn_readfirstlane(wm[M_EDA]);
+        const uint32_t edB = __builtin_amdgcn_readfirstlane(wm[M_EDB]);
         // selectors extracting slot L0 (stream 1's first byte) from T: slot j is byte j/4 of
         // T[j%4], i.e. byte (j%4 & 1)*4 + j/4 of perm(T[1],T[0]) or perm(T[3],T[2])
         uint32_t fsA = 0x0c0c0c0cu, fsB = 0x0c0c0c0cu;
@@ -656,7 +682,7 @@ __global__ __launch_bounds__(TEAM) void tdt_encode_kernel(EncodeArgs a) {
             else if (f == 1) v = n32;
             else if (f == 2) v = ns;
             else if (f == 3 || f == 4) v = WS;
-            else v = misc[M_MAP + (f - 5)];
+            else v = wm[M_MAP + (f - 5)];
             dst[t] = (uint8_t)(v >> sh);
         }
         if (tid < 8) {

@@ -2,6 +2,8 @@
 reference codec, and against the CPU oracle on seeded inputs.  Bit-exact everywhere: this
 is byte/integer work (the only floating point, the entropy decision, is restated
 bit-exactly; tests/test_log2_restatement.py)."""
+import struct
+
 import numpy as np
 import pytest
 
@@ -405,3 +407,65 @@ def test_slotted_capacity_and_errors():
     assert list(dst.cpu().numpy()[:3]) == [0, 2, 0]
     assert list(dln.cpu().numpy()[:3]) == [10, 0, 0]
     assert back.cpu().numpy()[:10].tobytes() == bytes(range(10))
+
+
+def _craft_blob(rng, orig, ws, mapping, stream_fill):
+    """A valid TDT blob (tdt_compression.hpp:81-117 layout) with arbitrary RLE streams:
+    stream_fill(c, need) returns the pair bytes of stream c (may be short, long, contain count 0
+    pairs or an odd trailing byte)."""
+    ns = max(mapping) + 1
+    wc = orig // ws
+    hdr = struct.pack("<5I", 0x54445444, orig, ns, ws, ws) + struct.pack("<%di" % ws, *mapping)
+    body = b""
+    for c in range(ns):
+        need = wc * mapping.count(c)
+        s = stream_fill(c, need)
+        body += struct.pack("<I", len(s)) + s
+    return hdr + body
+
+
+def _pairs(rng, total, zero_frac=0.0, maxrun=255, odd=False):
+    out = bytearray()
+    left = total
+    while left > 0:
+        if zero_frac and rng.random() < zero_frac:
+            out += bytes([0, int(rng.integers(0, 256))])
+            continue
+        c = int(min(left, rng.integers(1, maxrun + 1)))
+        out += bytes([c, int(rng.integers(0, 256))])
+        left -= c
+    if odd:
+        out += bytes([int(rng.integers(1, 256))])
+    return bytes(out)
+
+
+def test_decode_crafted_fast_path(orc):
+    """Decoder windows/blocks: streams shorter or longer than needed, count-0 pairs, odd
+    trailing bytes, 1 and 2 referenced streams, messages spanning many windows (head-array
+    generations), run lengths from 1 to 255; compared with the oracle's decode."""
+    rng = np.random.default_rng(31)
+    blobs = []
+    maps = [[0, 0, 0, 0], [1, 1, 0, 0], [0, 1, 1, 1], [1, 0, 0, 0], [0, 1, 0, 1], [1, 1, 1, 0]]
+    for i in range(60):
+        orig = int(rng.choice([64, 1024, 4096, 20000, 65536, 65540, 140000]))
+        mp = maps[i % len(maps)]
+        mode = i % 5
+        maxrun = int(rng.choice([1, 2, 3, 8, 255]))
+
+        def fill(c, need, mode=mode, maxrun=maxrun):
+            if mode == 0:
+                return _pairs(rng, need, maxrun=maxrun)
+            if mode == 1:  # short stream: leaves zeros
+                return _pairs(rng, int(need * rng.random()), maxrun=maxrun)
+            if mode == 2:  # long stream: extra ignored
+                return _pairs(rng, need + int(rng.integers(1, 3000)), maxrun=maxrun)
+            if mode == 3:
+                return _pairs(rng, need, zero_frac=0.2, maxrun=maxrun, odd=True)
+            return _pairs(rng, need // 2, maxrun=maxrun, odd=True)
+        blobs.append(_craft_blob(rng, orig, 4, mp, fill))
+    codec = make_codec()
+    got, st = decode_list(codec, blobs)
+    for i, b in enumerate(blobs):
+        s, want = orc.decode(b)
+        assert st[i] == s == 0, (i, st[i], s)
+        assert got[i] == want, f"crafted blob {i}"
