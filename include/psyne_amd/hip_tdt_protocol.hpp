@@ -170,6 +170,7 @@ public:
         return tdt_decode_batch(ctx_, d_in, d_in_off, n, d_out, cap, d_out_off, d_status, stream);
     }
     tdt_ctx *context() { return ctx_; }
+    int word_size() const { return config_.word_size; }
 
 private:
     void push_metrics() { tdt_ctx_set_metrics(ctx_, bandwidth_mbps_.load(), latency_ms_.load(), cpu_usage_.load()); }

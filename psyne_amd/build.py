@@ -41,6 +41,8 @@ def build(force: bool = False, verbose: bool = False) -> pathlib.Path:
 
 CPP_TEST_SRC = ROOT / "tests" / "cpp" / "test_protocol.cpp"
 CPP_TEST_BIN = ROOT / "tests" / "cpp" / "test_protocol"
+LOOPBACK_SRC = ROOT / "tools" / "tcp_loopback.cpp"
+LOOPBACK_BIN = ROOT / "tools" / "tcp_loopback"
 SELFTEST_SRC = ROOT / "tests" / "native" / "selftest.hip"
 SELFTEST_LIB = ROOT / "tests" / "native" / "libtdt_selftest.so"
 
@@ -52,6 +54,15 @@ def build_tests(verbose: bool = False):
             LIB.stat().st_mtime):
         cmd = ["g++", "-std=c++20", "-O2", "-I", str(ROOT / "include"), str(CPP_TEST_SRC), "-o", str(CPP_TEST_BIN),
                "-L", str(PKG), "-lpsyne_tdt", "-Wl,-rpath," + str(PKG), "-Wl,-rpath,$ORIGIN/../../psyne_amd"]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.check_call(cmd)
+    hdrs = [ROOT / "include/psyne_amd/hip_tdt_protocol.hpp", ROOT / "include/psyne_amd/tdt_substrate.hpp"]
+    if not LOOPBACK_BIN.exists() or LOOPBACK_BIN.stat().st_mtime < max(
+            [LOOPBACK_SRC.stat().st_mtime, LIB.stat().st_mtime] + [h.stat().st_mtime for h in hdrs]):
+        cmd = ["g++", "-std=c++20", "-O2", "-I", str(ROOT / "include"), str(LOOPBACK_SRC), "-o", str(LOOPBACK_BIN),
+               "-L", str(PKG), "-lpsyne_tdt", "-pthread", "-Wl,-rpath," + str(PKG),
+               "-Wl,-rpath,$ORIGIN/../psyne_amd"]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.check_call(cmd)

@@ -48,9 +48,20 @@ struct tdt_ctx {
     // workspace: [0..64) counters (ticket, timeout), then one u64 look-back word per message
     uint8_t *ws = nullptr;
     size_t ws_bytes = 0;
-    // host-path device buffers
+    // host-path device buffers (tdt_analyze_host)
     uint8_t *h_dev = nullptr;
     size_t h_dev_bytes = 0;
+    // host pipeline (tdt_encode_host / tdt_decode_host): two slots, each with its own stream,
+    // device buffer (input, offsets, output, status, look-back workspace) and pinned offsets
+    struct HostSlot {
+        hipStream_t stream = nullptr;
+        hipEvent_t ev = nullptr;
+        uint8_t *dev = nullptr;
+        size_t dev_bytes = 0;
+        uint64_t *pin = nullptr;  // pinned: in_off (n+1) | out_off (n+1) | status (n, int32 pairs)
+        size_t pin_words = 0;
+    } hs[2];
+    std::mutex hmu;
 };
 
 namespace {
@@ -104,18 +115,23 @@ int launch_encode(tdt_ctx *c, psy::EncodeArgs a, hipStream_t s) {
     return set_err(TDT_E_UNSUPPORTED, "word_size not supported on the GPU path");
 }
 
-int prep(tdt_ctx *c, uint32_t n_msgs, hipStream_t s) {
+// Zero the counters + look-back words of a batch; `wsp` = an explicit workspace (host
+// pipeline slots) or null for the context's own.
+int prep(tdt_ctx *c, uint32_t n_msgs, hipStream_t s, uint8_t *&wsp) {
     HIPCHK(hipSetDevice(c->device));
-    int st = ensure_ws(c, n_msgs);
-    if (st) return st;
-    HIPCHK(hipMemsetAsync(c->ws, 0, kCounterBytes + 8ull * n_msgs, s));
+    if (!wsp) {
+        int st = ensure_ws(c, n_msgs);
+        if (st) return st;
+        wsp = c->ws;
+    }
+    HIPCHK(hipMemsetAsync(wsp, 0, kCounterBytes + 8ull * n_msgs, s));
     return TDT_OK;
 }
 
 int encode_common(tdt_ctx *c, int mode, const uint8_t *d_in, const uint64_t *d_in_off, uint32_t n_msgs,
                   const int32_t *d_mapping, uint8_t *d_out, uint64_t out_cap, uint64_t *d_out_off,
                   int32_t *d_status, uint32_t *d_hist, double *d_ent, int32_t *d_map, void *stream,
-                  const uint64_t *d_slot_off = nullptr, uint64_t *d_out_len = nullptr) {
+                  const uint64_t *d_slot_off = nullptr, uint64_t *d_out_len = nullptr, uint8_t *wsp = nullptr) {
     if (!c) return set_err(TDT_E_ARG, "null context");
     if (n_msgs == 0) return TDT_OK;
     if (!d_in_off) return set_err(TDT_E_ARG, "null input offsets");  // d_in may be null: all-empty batch
@@ -123,8 +139,9 @@ int encode_common(tdt_ctx *c, int mode, const uint8_t *d_in, const uint64_t *d_i
     if (mode != psy::MODE_ANALYZE && (!d_out || (!slotted && !d_out_off))) return set_err(TDT_E_ARG, "null output");
     if (mode == psy::MODE_MAPPED && !d_mapping) return set_err(TDT_E_ARG, "null mapping");
     hipStream_t s = (hipStream_t)stream;
-    std::lock_guard<std::mutex> lk(c->mu);
-    int st = prep(c, n_msgs, s);
+    std::unique_lock<std::mutex> lk(c->mu, std::defer_lock);
+    if (!wsp) lk.lock();  // pipeline slots own their workspace
+    int st = prep(c, n_msgs, s, wsp);
     if (st) return st;
     psy::EncodeArgs a{};
     a.in = d_in;
@@ -138,9 +155,9 @@ int encode_common(tdt_ctx *c, int mode, const uint8_t *d_in, const uint64_t *d_i
     a.hist_out = d_hist;
     a.ent_out = d_ent;
     a.map_out = d_map;
-    a.ticket = reinterpret_cast<uint32_t *>(c->ws);
-    a.errflags = reinterpret_cast<uint32_t *>(c->ws) + 1;
-    a.lookback = reinterpret_cast<uint64_t *>(c->ws + kCounterBytes);
+    a.ticket = reinterpret_cast<uint32_t *>(wsp);
+    a.errflags = reinterpret_cast<uint32_t *>(wsp) + 1;
+    a.lookback = reinterpret_cast<uint64_t *>(wsp + kCounterBytes);
     a.min_tensor = c->cfg.min_tensor_size;
     a.policy_on = policy_on(c) ? 1 : 0;
     a.slot_off = d_slot_off;
@@ -160,7 +177,7 @@ int encode_common(tdt_ctx *c, int mode, const uint8_t *d_in, const uint64_t *d_i
 int decode_common(tdt_ctx *c, bool sizes_only, const uint8_t *d_in, const uint64_t *d_in_off, uint32_t n_msgs,
                   uint8_t *d_out, uint64_t out_cap, uint64_t *d_out_off, uint64_t *d_sizes, int32_t *d_status,
                   void *stream, const uint64_t *d_slot_off = nullptr, uint64_t *d_out_len = nullptr,
-                  const uint64_t *d_in_len = nullptr) {
+                  const uint64_t *d_in_len = nullptr, uint8_t *wsp = nullptr) {
     if (!c) return set_err(TDT_E_ARG, "null context");
     if (n_msgs == 0) return TDT_OK;
     if (!d_in_off) return set_err(TDT_E_ARG, "null input offsets");
@@ -168,8 +185,9 @@ int decode_common(tdt_ctx *c, bool sizes_only, const uint8_t *d_in, const uint64
     if (!sizes_only && !slotted && !d_out_off) return set_err(TDT_E_ARG, "null output offsets");
     if (sizes_only && !d_sizes) return set_err(TDT_E_ARG, "null sizes");
     hipStream_t s = (hipStream_t)stream;
-    std::lock_guard<std::mutex> lk(c->mu);
-    int st = prep(c, n_msgs, s);
+    std::unique_lock<std::mutex> lk(c->mu, std::defer_lock);
+    if (!wsp) lk.lock();
+    int st = prep(c, n_msgs, s, wsp);
     if (st) return st;
     psy::DecodeArgs a{};
     a.in = d_in;
@@ -180,9 +198,9 @@ int decode_common(tdt_ctx *c, bool sizes_only, const uint8_t *d_in, const uint64
     a.out_off = d_out_off;
     a.status = d_status;
     a.sizes_out = d_sizes;
-    a.ticket = reinterpret_cast<uint32_t *>(c->ws);
-    a.errflags = reinterpret_cast<uint32_t *>(c->ws) + 1;
-    a.lookback = reinterpret_cast<uint64_t *>(c->ws + kCounterBytes);
+    a.ticket = reinterpret_cast<uint32_t *>(wsp);
+    a.errflags = reinterpret_cast<uint32_t *>(wsp) + 1;
+    a.lookback = reinterpret_cast<uint64_t *>(wsp + kCounterBytes);
     a.slot_off = d_slot_off;
     a.out_len = d_out_len;
     a.in_len = d_in_len;
@@ -206,6 +224,207 @@ int ensure_host_dev(tdt_ctx *c, size_t bytes) {
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
+// ---------------------------------------------------------------------------------------
+// Host pipeline (the TCP socket-buffer case).  The batch is cut into chunks of whole
+// messages (<= kHostChunk input bytes); chunk c runs on slot c % 2 — its own stream, device
+// buffer and look-back workspace — as H2D(input, offsets) → batch kernel → D2H.  While the
+// host waits for chunk c's output size (encode: the compacted size is only known after the
+// kernel), chunk c + 1's copies and kernel are already queued on the other stream, so PCIe
+// transfers in both directions overlap the kernels.
+constexpr uint64_t kHostChunk = 256ull << 20;
+
+int ensure_slot(tdt_ctx *c, int k, size_t dev_bytes, size_t pin_words) {
+    auto &h = c->hs[k];
+    if (!h.stream) {
+        HIPCHK(hipStreamCreateWithFlags(&h.stream, hipStreamNonBlocking));
+        HIPCHK(hipEventCreateWithFlags(&h.ev, hipEventDisableTiming));
+    }
+    if (dev_bytes > h.dev_bytes) {
+        if (h.dev) HIPCHK(hipFree(h.dev));
+        h.dev = nullptr;
+        h.dev_bytes = 0;
+        HIPCHK(hipMalloc(&h.dev, dev_bytes));
+        h.dev_bytes = dev_bytes;
+    }
+    if (pin_words > h.pin_words) {
+        if (h.pin) HIPCHK(hipHostFree(h.pin));
+        h.pin = nullptr;
+        h.pin_words = 0;
+        HIPCHK(hipHostMalloc(&h.pin, 8 * pin_words, hipHostMallocDefault));
+        h.pin_words = pin_words;
+    }
+    return TDT_OK;
+}
+
+struct Chunk {
+    uint32_t m0 = 0, n = 0;
+    uint64_t in_bytes = 0, cap = 0;
+    size_t o_off = 0, o_out = 0, o_ooff = 0, o_st = 0, o_ws = 0;
+};
+
+Chunk plan_chunk(const uint64_t *h_in_off, uint32_t m0, uint32_t n_msgs, bool encode, int ws,
+                 const uint64_t *dec_sizes) {
+    Chunk k;
+    k.m0 = m0;
+    uint32_t m = m0;
+    uint64_t cap = 0;
+    while (m < n_msgs) {
+        const uint64_t len = h_in_off[m + 1] - h_in_off[m];
+        if (m > m0 && h_in_off[m + 1] - h_in_off[m0] > kHostChunk) break;
+        cap += encode ? tdt_encode_bound(len, ws) : dec_sizes[m];
+        ++m;
+    }
+    k.n = m - m0;
+    k.in_bytes = h_in_off[m] - h_in_off[m0];
+    k.cap = cap;
+    k.o_off = align_up(k.in_bytes, 256);
+    k.o_out = align_up(k.o_off + 8ull * (k.n + 1), 256);
+    k.o_ooff = align_up(k.o_out + std::max<uint64_t>(cap, 1), 256);
+    k.o_st = align_up(k.o_ooff + 8ull * (k.n + 1), 256);
+    k.o_ws = align_up(k.o_st + 4ull * k.n, 256);
+    return k;
+}
+
+size_t chunk_dev_bytes(const Chunk &k) { return k.o_ws + kCounterBytes + 8ull * (k.n + 1); }
+
+// decode: the decoded size of every blob from its header (the kernel validates; a blob it
+// rejects gets 0 and its bytes are dropped when the output is compacted)
+uint64_t host_decoded_size(const uint8_t *b, uint64_t len) {
+    if (len < 4) return 0;
+    uint32_t magic;
+    std::memcpy(&magic, b, 4);
+    if (magic == psy::kMagicUNCP) return len - 4;
+    if (magic != psy::kMagicTDT || len < 8) return 0;
+    uint32_t orig;
+    std::memcpy(&orig, b + 4, 4);
+    return orig;
+}
+
+int host_encode(tdt_ctx *c, const uint8_t *h_in, const uint64_t *h_in_off, uint32_t n_msgs, uint8_t *h_out,
+                uint64_t out_cap, uint64_t *h_out_off, int32_t *h_status) {
+    const int ws = c->cfg.word_size;
+    std::vector<Chunk> ch;
+    for (uint32_t m = 0; m < n_msgs;) {
+        ch.push_back(plan_chunk(h_in_off, m, n_msgs, true, ws, nullptr));
+        m += ch.back().n;
+    }
+    uint64_t base = 0;  // output bytes of the chunks finished so far
+    bool capacity = false;
+    auto issue = [&](size_t ci) -> int {
+        const Chunk &k = ch[ci];
+        auto &h = c->hs[ci & 1];
+        int st = ensure_slot(c, (int)(ci & 1), chunk_dev_bytes(k), 2ull * (k.n + 1));
+        if (st) return st;
+        HIPCHK(hipStreamSynchronize(h.stream));  // the slot's previous chunk is done with its buffers
+        uint64_t *pin_in = h.pin;
+        const uint64_t b0 = h_in_off[k.m0];
+        for (uint32_t i = 0; i <= k.n; ++i) pin_in[i] = h_in_off[k.m0 + i] - b0;
+        uint8_t *d = h.dev;
+        auto *doff = reinterpret_cast<uint64_t *>(d + k.o_off);
+        auto *dooff = reinterpret_cast<uint64_t *>(d + k.o_ooff);
+        auto *dst = reinterpret_cast<int32_t *>(d + k.o_st);
+        HIPCHK(hipMemcpyAsync(d, h_in + b0, k.in_bytes, hipMemcpyHostToDevice, h.stream));
+        HIPCHK(hipMemcpyAsync(doff, pin_in, 8ull * (k.n + 1), hipMemcpyHostToDevice, h.stream));
+        st = encode_common(c, psy::MODE_ENCODE, d, doff, k.n, nullptr, d + k.o_out, k.cap, dooff, dst, nullptr, nullptr,
+                           nullptr, h.stream, nullptr, nullptr, d + k.o_ws);
+        if (st) return st;
+        HIPCHK(hipMemcpyAsync(h.pin + (k.n + 1), dooff, 8ull * (k.n + 1), hipMemcpyDeviceToHost, h.stream));
+        if (h_status) HIPCHK(hipMemcpyAsync(h_status + k.m0, dst, 4ull * k.n, hipMemcpyDeviceToHost, h.stream));
+        HIPCHK(hipEventRecord(h.ev, h.stream));
+        return TDT_OK;
+    };
+    // chunk ci's compacted size is known once its event fires; then queue its data D2H
+    auto finish = [&](size_t ci) -> int {
+        const Chunk &k = ch[ci];
+        auto &h = c->hs[ci & 1];
+        HIPCHK(hipEventSynchronize(h.ev));
+        const uint64_t *pin_out = h.pin + (k.n + 1);
+        const uint64_t total = pin_out[k.n];
+        if (capacity || base + total > out_cap) capacity = true;
+        for (uint32_t i = 0; i < k.n; ++i) h_out_off[k.m0 + i] = base + (capacity ? 0 : pin_out[i]);
+        if (!capacity && total)
+            HIPCHK(hipMemcpyAsync(h_out + base, h.dev + k.o_out, total, hipMemcpyDeviceToHost, h.stream));
+        if (!capacity) base += total;
+        return TDT_OK;
+    };
+    for (size_t ci = 0; ci < ch.size(); ++ci) {
+        int st = issue(ci);
+        if (!st && ci > 0) st = finish(ci - 1);
+        if (st) return st;
+    }
+    int st = finish(ch.size() - 1);
+    if (st) return st;
+    for (auto &h : c->hs)
+        if (h.stream) HIPCHK(hipStreamSynchronize(h.stream));
+    h_out_off[n_msgs] = base;
+    if (capacity) return set_err(TDT_E_CAPACITY, "host output capacity exceeded");
+    return TDT_OK;
+}
+
+int host_decode(tdt_ctx *c, const uint8_t *h_in, const uint64_t *h_in_off, uint32_t n_msgs, uint8_t *h_out,
+                uint64_t out_cap, uint64_t *h_out_off, int32_t *h_status) {
+    // decoded sizes from the headers → every chunk's output offsets are known up front: the
+    // decode is slotted at those offsets and every copy is queued without waiting
+    std::vector<uint64_t> dsz(n_msgs);
+    uint64_t need = 0;
+    for (uint32_t i = 0; i < n_msgs; ++i) {
+        dsz[i] = host_decoded_size(h_in + h_in_off[i], h_in_off[i + 1] - h_in_off[i]);
+        need += dsz[i];
+    }
+    if (need > out_cap) return set_err(TDT_E_CAPACITY, "host output capacity exceeded");
+    std::vector<Chunk> ch;
+    for (uint32_t m = 0; m < n_msgs;) {
+        ch.push_back(plan_chunk(h_in_off, m, n_msgs, false, c->cfg.word_size, dsz.data()));
+        m += ch.back().n;
+    }
+    std::vector<uint64_t> lens(n_msgs);
+    std::vector<int32_t> stv(n_msgs);
+    uint64_t base = 0;
+    for (size_t ci = 0; ci < ch.size(); ++ci) {
+        const Chunk &k = ch[ci];
+        auto &h = c->hs[ci & 1];
+        int st = ensure_slot(c, (int)(ci & 1), chunk_dev_bytes(k) + 8ull * k.n, 2ull * (k.n + 1));
+        if (st) return st;
+        HIPCHK(hipStreamSynchronize(h.stream));
+        uint64_t *pin_in = h.pin, *pin_slot = h.pin + (k.n + 1);
+        const uint64_t b0 = h_in_off[k.m0];
+        uint64_t acc = 0;
+        for (uint32_t i = 0; i <= k.n; ++i) {
+            pin_in[i] = h_in_off[k.m0 + i] - b0;
+            pin_slot[i] = acc;
+            if (i < k.n) acc += dsz[k.m0 + i];
+        }
+        uint8_t *d = h.dev;
+        auto *doff = reinterpret_cast<uint64_t *>(d + k.o_off);
+        auto *dslot = reinterpret_cast<uint64_t *>(d + k.o_ooff);
+        auto *dst = reinterpret_cast<int32_t *>(d + k.o_st);
+        auto *dlen = reinterpret_cast<uint64_t *>(d + chunk_dev_bytes(k));
+        HIPCHK(hipMemcpyAsync(d, h_in + b0, k.in_bytes, hipMemcpyHostToDevice, h.stream));
+        HIPCHK(hipMemcpyAsync(doff, pin_in, 8ull * (k.n + 1), hipMemcpyHostToDevice, h.stream));
+        HIPCHK(hipMemcpyAsync(dslot, pin_slot, 8ull * (k.n + 1), hipMemcpyHostToDevice, h.stream));
+        st = decode_common(c, false, d, doff, k.n, d + k.o_out, 0, nullptr, nullptr, dst, h.stream, dslot, dlen,
+                           nullptr, d + k.o_ws);
+        if (st) return st;
+        if (acc) HIPCHK(hipMemcpyAsync(h_out + base, d + k.o_out, acc, hipMemcpyDeviceToHost, h.stream));
+        HIPCHK(hipMemcpyAsync(lens.data() + k.m0, dlen, 8ull * k.n, hipMemcpyDeviceToHost, h.stream));
+        HIPCHK(hipMemcpyAsync(stv.data() + k.m0, dst, 4ull * k.n, hipMemcpyDeviceToHost, h.stream));
+        base += acc;
+    }
+    for (auto &h : c->hs)
+        if (h.stream) HIPCHK(hipStreamSynchronize(h.stream));
+    // offsets; blobs the kernel rejected (status != OK, length 0) leave a gap: compact it
+    uint64_t w = 0, r = 0;
+    for (uint32_t i = 0; i < n_msgs; ++i) {
+        h_out_off[i] = w;
+        if (lens[i] && w != r) std::memmove(h_out + w, h_out + r, lens[i]);
+        w += lens[i];
+        r += dsz[i];
+        if (h_status) h_status[i] = stv[i];
+    }
+    h_out_off[n_msgs] = w;
+    return TDT_OK;
+}
+
 int host_path(tdt_ctx *c, bool encode, const uint8_t *h_in, const uint64_t *h_in_off, uint32_t n_msgs,
               uint8_t *h_out, uint64_t out_cap, uint64_t *h_out_off, int32_t *h_status) {
     if (!c) return set_err(TDT_E_ARG, "null context");
@@ -213,48 +432,11 @@ int host_path(tdt_ctx *c, bool encode, const uint8_t *h_in, const uint64_t *h_in
         if (h_out_off) h_out_off[0] = 0;
         return TDT_OK;
     }
+    if (!h_in_off || !h_out_off) return set_err(TDT_E_ARG, "null offsets");
     HIPCHK(hipSetDevice(c->device));
-    const uint64_t in_bytes = h_in_off[n_msgs] - h_in_off[0];
-    const size_t o_in = 0;
-    const size_t o_off = align_up(o_in + in_bytes, 256);
-    const size_t o_out = align_up(o_off + 8ull * (n_msgs + 1), 256);
-    const size_t o_ooff = align_up(o_out + out_cap, 256);
-    const size_t o_st = align_up(o_ooff + 8ull * (n_msgs + 1), 256);
-    const size_t total = align_up(o_st + 4ull * n_msgs, 256);
-    int st;
-    {
-        std::lock_guard<std::mutex> lk(c->mu);
-        st = ensure_host_dev(c, total);
-    }
-    if (st) return st;
-    uint8_t *d = c->h_dev;
-    hipStream_t s = nullptr;
-    HIPCHK(hipMemcpyAsync(d + o_in, h_in + h_in_off[0], in_bytes, hipMemcpyHostToDevice, s));
-    // offsets rebased to 0
-    uint64_t *tmp = new uint64_t[n_msgs + 1];
-    for (uint32_t i = 0; i <= n_msgs; ++i) tmp[i] = h_in_off[i] - h_in_off[0];
-    hipError_t e = hipMemcpyAsync(d + o_off, tmp, 8ull * (n_msgs + 1), hipMemcpyHostToDevice, s);
-    if (e == hipSuccess) e = hipStreamSynchronize(s);
-    delete[] tmp;
-    if (e != hipSuccess) return set_err(TDT_E_HIP, hipGetErrorString(e));
-    if (encode)
-        st = encode_common(c, psy::MODE_ENCODE, d + o_in, reinterpret_cast<uint64_t *>(d + o_off), n_msgs, nullptr,
-                           d + o_out, out_cap, reinterpret_cast<uint64_t *>(d + o_ooff),
-                           reinterpret_cast<int32_t *>(d + o_st), nullptr, nullptr, nullptr, s);
-    else
-        st = decode_common(c, false, d + o_in, reinterpret_cast<uint64_t *>(d + o_off), n_msgs, d + o_out, out_cap,
-                           reinterpret_cast<uint64_t *>(d + o_ooff), nullptr, reinterpret_cast<int32_t *>(d + o_st),
-                           s);
-    if (st) return st;
-    HIPCHK(hipMemcpyAsync(h_out_off, d + o_ooff, 8ull * (n_msgs + 1), hipMemcpyDeviceToHost, s));
-    if (h_status) HIPCHK(hipMemcpyAsync(h_status, d + o_st, 4ull * n_msgs, hipMemcpyDeviceToHost, s));
-    uint32_t flags = 0;
-    HIPCHK(hipMemcpyAsync(&flags, c->ws + 4, 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
-    if (flags) return set_err(TDT_E_HIP, "device error flags " + std::to_string(flags));
-    const uint64_t produced = std::min<uint64_t>(h_out_off[n_msgs], out_cap);
-    if (produced) HIPCHK(hipMemcpy(h_out, d + o_out, produced, hipMemcpyDeviceToHost));
-    return TDT_OK;
+    std::lock_guard<std::mutex> lk(c->hmu);  // the pipeline slots belong to the context
+    return encode ? host_encode(c, h_in, h_in_off, n_msgs, h_out, out_cap, h_out_off, h_status)
+                  : host_decode(c, h_in, h_in_off, n_msgs, h_out, out_cap, h_out_off, h_status);
 }
 
 }  // namespace
@@ -292,6 +474,13 @@ void tdt_ctx_destroy(tdt_ctx *ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->ws) (void)hipFree(ctx->ws);
     if (ctx->h_dev) (void)hipFree(ctx->h_dev);
+    for (auto &h : ctx->hs) {
+        if (h.stream) (void)hipStreamSynchronize(h.stream);
+        if (h.dev) (void)hipFree(h.dev);
+        if (h.pin) (void)hipHostFree(h.pin);
+        if (h.ev) (void)hipEventDestroy(h.ev);
+        if (h.stream) (void)hipStreamDestroy(h.stream);
+    }
     delete ctx;
 }
 
