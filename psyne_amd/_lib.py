@@ -6,6 +6,7 @@ raises.  Pointers passed to the batch entry points are device pointers.
 from __future__ import annotations
 
 import ctypes as C
+import os
 import pathlib
 
 LIB_PATH = pathlib.Path(__file__).resolve().parent / "libpsyne_tdt.so"
@@ -61,7 +62,8 @@ def load(path: pathlib.Path | None = None) -> C.CDLL:
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = pathlib.Path(path or LIB_PATH)
+    # PSYNE_TDT_LIB: an alternative build of the same HIP library (diagnostic experiments)
+    p = pathlib.Path(path or os.environ.get("PSYNE_TDT_LIB") or LIB_PATH)
     if not p.exists():
         raise RuntimeError(f"{p} not built: run `python -m psyne_amd.build` (hipcc --offload-arch=gfx950)")
     lib = C.CDLL(str(p))

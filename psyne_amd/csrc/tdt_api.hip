@@ -95,10 +95,16 @@ int launch_encode_t(psy::EncodeArgs a, hipStream_t s) {
     return TDT_OK;
 }
 
+// messages > 4 KiB: TEAM threads per message, G resident rounds per wave (64 KiB resident)
+#ifndef PSY_BIG_TEAM
+#define PSY_BIG_TEAM 512
+#define PSY_BIG_G 8
+#endif
+
 template <int WS, int MODE, int LB>
 int launch_encode_ws(psy::EncodeArgs a, bool small, hipStream_t s) {
     if (small) return launch_encode_t<WS, 64, 4, MODE, LB>(a, s);
-    return launch_encode_t<WS, 512, 8, MODE, LB>(a, s);
+    return launch_encode_t<WS, PSY_BIG_TEAM, PSY_BIG_G, MODE, LB>(a, s);
 }
 
 // LB: compacted output (look-back) vs slotted output
@@ -106,11 +112,15 @@ template <int MODE, int LB>
 int launch_encode(tdt_ctx *c, psy::EncodeArgs a, hipStream_t s) {
     const bool small = c->size_hint.load() <= 4096;
     switch (c->cfg.word_size) {
+#ifdef PSY_FAST_BUILD  // diagnostic builds: word_size 4 only
+        case 4: return launch_encode_ws<4, MODE, LB>(a, small, s);
+#else
         case 1: return launch_encode_ws<1, MODE, LB>(a, small, s);
         case 2: return launch_encode_ws<2, MODE, LB>(a, small, s);
         case 4: return launch_encode_ws<4, MODE, LB>(a, small, s);
         case 8: return launch_encode_ws<8, MODE, LB>(a, small, s);
         case 16: return launch_encode_ws<16, MODE, LB>(a, small, s);
+#endif
     }
     return set_err(TDT_E_UNSUPPORTED, "word_size not supported on the GPU path");
 }

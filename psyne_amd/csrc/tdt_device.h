@@ -34,6 +34,11 @@ __device__ unsigned long long psy_prof[32];
 #define PSY_PROF_BEGIN() ((void)0)
 #define PSY_PROF_MARK(i) ((void)0)
 #endif
+#ifdef PSY_ASM_MARKS
+#define PSY_ASM_ROUND(p) asm volatile(";@@ROUND " #p ::)
+#else
+#define PSY_ASM_ROUND(p) ((void)0)
+#endif
 
 template <int CTRL, int ROWMASK = 0xf, int BANKMASK = 0xf>
 __device__ __forceinline__ uint32_t dpp_mov(uint32_t x) {
@@ -49,9 +54,30 @@ struct OpMax {
     __device__ __forceinline__ static uint32_t f(uint32_t a, uint32_t b) { return a > b ? a : b; }
 };
 
+// DPP move whose disabled / out-of-row lanes return x itself: the identity for idempotent
+// operators (max), so no zero-initialised register is needed.
+template <int CTRL, int ROWMASK = 0xf, int BANKMASK = 0xf>
+__device__ __forceinline__ uint32_t dpp_mov_self(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, CTRL, ROWMASK, BANKMASK, false);
+}
+
+template <class Op>
+struct ScanIdem {
+    static constexpr bool value = false;
+};
+
 // Inclusive wave64 scan with identity 0.
 template <class Op>
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+    if constexpr (ScanIdem<Op>::value) {
+        x = Op::f(x, dpp_mov_self<0x111>(x));
+        x = Op::f(x, dpp_mov_self<0x112>(x));
+        x = Op::f(x, dpp_mov_self<0x114>(x));
+        x = Op::f(x, dpp_mov_self<0x118>(x));
+        x = Op::f(x, dpp_mov_self<0x142, 0xa>(x));
+        x = Op::f(x, dpp_mov_self<0x143, 0xc>(x));
+        return x;
+    }
     x = Op::f(x, dpp_mov<0x111>(x));       // row_shr:1
     x = Op::f(x, dpp_mov<0x112>(x));       // row_shr:2
     x = Op::f(x, dpp_mov<0x114>(x));       // row_shr:4
@@ -83,6 +109,14 @@ __device__ __forceinline__ uint32_t pk_max_u16(uint32_t a, uint32_t b) {
 }
 struct OpPkMax {
     __device__ __forceinline__ static uint32_t f(uint32_t a, uint32_t b) { return pk_max_u16(a, b); }
+};
+template <>
+struct ScanIdem<OpMax> {
+    static constexpr bool value = true;
+};
+template <>
+struct ScanIdem<OpPkMax> {
+    static constexpr bool value = true;
 };
 
 // v_ffbh_u32 with its hardware semantics (count of leading zeros, 0xffffffff for 0), so the

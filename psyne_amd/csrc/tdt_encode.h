@@ -91,16 +91,18 @@ struct EncLayout {
     static constexpr int WSTAGE = 2 * WREGION + 16;  // both streams + a junk pair, per wave
     static constexpr int STAGE = W * WSTAGE;
     static constexpr int TERMS = TB * 256 * 16;
-    // log2 tables (2 KiB) live in the union after the terms: both are dead by pass B
-    static constexpr int TERMS_LOG2 = TERMS + 2048;
-    static constexpr int UNION = STAGE > TERMS_LOG2 ? STAGE : TERMS_LOG2;
+    // Two phases share one region: histogram + entropy terms + log2 tables (dead once the
+    // mapping is known) and pass B's per-wave staging windows.
+    static constexpr int ANALYSIS = HIST + TERMS + 2048;
+    static constexpr int REGION = STAGE > ANALYSIS ? STAGE : ANALYSIS;
     static constexpr int SLOTS = W * 8 * 4;
     static constexpr int MISC = 512;
-    static constexpr int WM = 128;  // per-wave mapping state (uint32)
+    static constexpr int WM = 128;  // mapping state (uint32)
     static constexpr int OFF_HIST = 0;
-    static constexpr int OFF_UNION = OFF_HIST + HIST;
-    static constexpr int OFF_LOG2 = OFF_UNION + TERMS;
-    static constexpr int OFF_SLOTS = OFF_UNION + UNION;
+    static constexpr int OFF_TERMS = HIST;
+    static constexpr int OFF_LOG2 = HIST + TERMS;
+    static constexpr int OFF_STAGE = 0;
+    static constexpr int OFF_SLOTS = REGION;
     static constexpr int OFF_MISC = OFF_SLOTS + SLOTS;
     static constexpr int OFF_WMISC = OFF_MISC + MISC;
     static constexpr int BYTES = OFF_WMISC + WM * 4;
@@ -139,8 +141,14 @@ __device__ __forceinline__ uint32_t spread2(uint32_t e) {
 // LB = 1: compacted output, offsets by decoupled look-back (out_off written);
 // LB = 0: slotted output at caller offsets (slot_off), lengths to out_len — no dependency
 //         between messages.
+// Occupancy target (min waves per SIMD): 3 workgroups of 512 per CU = 6 waves per SIMD.
+#ifndef PSY_ENC_WPE
+#define PSY_ENC_WPE 6
+#endif
+#define PSY_ENC_WAVES(TEAM) ((TEAM) >= 512 ? PSY_ENC_WPE : 1)
+
 template <int WS, int TEAM, int G, int MODE, int LB>
-__global__ __launch_bounds__(TEAM) void tdt_encode_kernel(EncodeArgs a) {
+__global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(EncodeArgs a) {
     using Lay = EncLayout<WS, TEAM>;
     constexpr int W = Lay::W;
     constexpr int WPG = Lay::WPG;
@@ -320,11 +328,16 @@ __global__ __launch_bounds__(TEAM) void tdt_encode_kernel(EncodeArgs a) {
             for (int i = 0; i < 16; ++i) {
                 const uint32_t v = (dw[i >> 2] >> (8 * (i & 3))) & 0xffu;
                 const uint32_t ad = v ? (v << (Lay::LOG_HC + 2)) + coff : zoff;
+#ifndef PSY_X_NOHIST
                 if (full || (uint32_t)i < vb)
+#else
+                if (vb == 12345u)
+#endif
                     atomicAdd(reinterpret_cast<uint32_t *>(smem + Lay::OFF_HIST + (i % WS) * Lay::PS * 4 + ad), 1u);
             }
         };
         for_rounds([&](uint32_t r, uint4 &d, uint32_t &, auto) __attribute__((always_inline)) {
+            PSY_ASM_ROUND(H);
             if (full_round(r)) hist_group(d, 16, true);
             else hist_group(d, vbytes(gw0 + r * 64 + lane), false);
         });
@@ -342,7 +355,7 @@ __global__ __launch_bounds__(TEAM) void tdt_encode_kernel(EncodeArgs a) {
         // (-prob, log2 prob) is computed in parallel (0, 0 for an empty bin, so the chain
         // needs no select: fma(0, 0, e) == e for the non-negative running sum); then in every
         // wave one lane per position runs the exact fma chain in bin order.
-        double *terms = reinterpret_cast<double *>(smem + Lay::OFF_UNION);
+        double *terms = reinterpret_cast<double *>(smem + Lay::OFF_TERMS);
         const double *ltab = reinterpret_cast<const double *>(smem + Lay::OFF_LOG2);
         const double total = (double)wc;
         for (int q0 = 0; q0 < WS; q0 += Lay::TB) {
@@ -582,6 +595,7 @@ __global__ __launch_bounds__(TEAM) void tdt_encode_kernel(EncodeArgs a) {
         {
             uint32_t edc = edc0;
             for_rounds([&](uint32_t r, uint4 &d, uint32_t &cm, auto res) __attribute__((always_inline)) {
+                PSY_ASM_ROUND(A1);
                 const uint32_t g = gw0 + r * 64 + lane;
                 uint32_t T[4];
                 tmat(d, T);
@@ -624,6 +638,7 @@ __global__ __launch_bounds__(TEAM) void tdt_encode_kernel(EncodeArgs a) {
             uint32_t rcarry[2] = {rin[0], rin[1]};
             uint32_t edc = edc0;
             for_rounds([&](uint32_t r, uint4 &d, uint32_t &cm, auto res) __attribute__((always_inline)) {
+                PSY_ASM_ROUND(A2);
                 const uint32_t g = gw0 + r * 64 + lane;
                 const uint32_t V = full_round(r) ? 0xffffu : vmask(vbytes(g));
                 uint32_t m;
@@ -696,7 +711,7 @@ __global__ __launch_bounds__(TEAM) void tdt_encode_kernel(EncodeArgs a) {
 
         // ---------------------------------------------------------- pass B: emit pairs
         // Wave-local from here on: per-wave LDS staging, no workgroup barrier.
-        const uint32_t wst = Lay::OFF_UNION + wv * Lay::WSTAGE;
+        const uint32_t wst = Lay::OFF_STAGE + wv * Lay::WSTAGE;
         uint32_t pr[2] = {(uint32_t)__builtin_amdgcn_readfirstlane(pin[0]), (uint32_t)__builtin_amdgcn_readfirstlane(pin[1])};
         // last chunk start + 1 before this wave: inside the run carried in (start rin - 1),
         // chunks start every 255 bytes (simple_rle_compress :568)
@@ -713,6 +728,10 @@ __global__ __launch_bounds__(TEAM) void tdt_encode_kernel(EncodeArgs a) {
         // Emit the pairs of round r: Tw its slot word, C its chunk-start mask, nxt63 the chunk
         // bits of the group after lane 63's (combined layout).
         auto emit = [&](uint32_t r, const uint4 &Tw, uint32_t C, uint32_t nxt63) __attribute__((always_inline)) {
+#ifdef PSY_X_NOEMIT
+            if (r < 100) return;
+#endif
+            PSY_ASM_ROUND(B);
             const uint32_t T[4] = {Tw.x, Tw.y, Tw.z, Tw.w};
             const uint32_t g = gw0 + r * 64 + lane;
             // the message does not end inside (or before the end of) this round
@@ -805,23 +824,32 @@ __global__ __launch_bounds__(TEAM) void tdt_encode_kernel(EncodeArgs a) {
 #pragma unroll
             for (int c = 0; c < 2; ++c) {
                 if (Ls[c] == 0) continue;
-                uint32_t len = 2u * ends[c];
+                const uint32_t len = 2u * ends[c];
+#ifdef PSY_GUARDS
                 if (len && sdata[c] + 2ull * k0c[c] + len > E) {  // never for a consistent round
                     if (lane == 0) atomicOr(a.errflags, 4u);
-                    len = 0;
+                    continue;
                 }
+#endif
                 if (len) {
-                    uint8_t *gd = dst + sdata[c] + 2ull * k0c[c];
+                    // The window is congruent (mod 16) with the destination: the unaligned head
+                    // and tail bytes go out in ONE byte-store instruction (lanes 0-15 head, lanes
+                    // 32-47 tail), the body as aligned 16-byte stores (at most 2 per lane).
+                    uint8_t *const gd = dst + sdata[c] + 2ull * k0c[c];
                     const uint32_t ra = (uint32_t)(gdst[c] & 15);
                     const uint32_t head0 = (16u - ra) & 15u;
                     const uint32_t head = head0 < len ? head0 : len;
-                    const uint32_t body = (len - head) & ~15u;
-                    if ((uint32_t)lane < head) gd[lane] = smem[rbs[c] + lane];
-                    for (uint32_t k = lane; k < body / 16; k += 64)
-                        *reinterpret_cast<uint4 *>(gd + head + 16 * k) =
-                            *reinterpret_cast<const uint4 *>(smem + rbs[c] + head + 16 * k);
-                    const uint32_t tail = len - head - body;
-                    if ((uint32_t)lane < tail) gd[head + body + lane] = smem[rbs[c] + head + body + lane];
+                    const uint32_t body16 = (len - head) >> 4;
+                    const uint32_t tail = len - head - 16u * body16;
+                    const uint32_t ht = (uint32_t)lane < 16u ? (uint32_t)lane : head + 16u * body16 + ((uint32_t)lane - 32u);
+                    if ((uint32_t)lane < head || ((uint32_t)lane - 32u) < tail) gd[ht] = smem[rbs[c] + ht];
+#pragma unroll
+                    for (uint32_t it = 0; it < 2; ++it) {
+                        const uint32_t k = (uint32_t)lane + 64u * it;
+                        if (k < body16)
+                            *reinterpret_cast<uint4 *>(gd + head + 16u * k) =
+                                *reinterpret_cast<const uint4 *>(smem + rbs[c] + head + 16u * k);
+                    }
                 }
                 pr[c] += (ptr >> (16 * c)) & 0xffffu;
                 const uint32_t ci = (rdlane(cinc, 63) >> (16 * c)) & 0xffffu;
