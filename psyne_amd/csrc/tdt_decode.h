@@ -266,7 +266,11 @@ __device__ __forceinline__ void decode_fast(uint32_t *misc, uint8_t *smem, const
             for (int h = 0; h < 2; ++h) {
                 const uint32_t rel = st[r][2 * j + h] - wstart;
                 const uint32_t slot = rel < wlen[r] ? rel : wlen[r];
+#ifndef PSY_X_NOKEYS
                 *reinterpret_cast<uint16_t *>(smem + hbase[r] + 2u * slot) = (uint16_t)(h ? (k >> 16) : k);
+#else
+                if (slot == 0xfffffu) *reinterpret_cast<uint16_t *>(smem + hbase[r]) = (uint16_t)k;
+#endif
             }
         }
     };
@@ -299,8 +303,12 @@ __device__ __forceinline__ void decode_fast(uint32_t *misc, uint8_t *smem, const
             const uint32_t g0 = gwin + rl * 64u;
             if (g0 >= ngroups) break;
             const uint32_t hoffb = fh + 2u * rl * 64u * fseg;
-            const uint4 h0 = *reinterpret_cast<const uint4 *>(smem + hoffb);
-            const uint4 h1 = *reinterpret_cast<const uint4 *>(smem + hoffb + 16);
+            // lanes 8-15 of every 16 read their second half first: with 32-byte lane rows the
+            // two ds_read_b128 are then bank-conflict-free (MI355X_MICROARCH.md §LDS groups)
+            const bool sw = (lane & 8u) != 0u;
+            const uint4 ha = *reinterpret_cast<const uint4 *>(smem + hoffb + (sw ? 16u : 0u));
+            const uint4 hb = *reinterpret_cast<const uint4 *>(smem + hoffb + (sw ? 0u : 16u));
+            const uint4 h0 = sw ? hb : ha, h1 = sw ? ha : hb;
             uint32_t x[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
             uint32_t m = pk_max_u16(pk_max_u16(pk_max_u16(x[0], x[1]), pk_max_u16(x[2], x[3])),
                                     pk_max_u16(pk_max_u16(x[4], x[5]), pk_max_u16(x[6], x[7])));
@@ -336,8 +344,18 @@ __device__ __forceinline__ void decode_fast(uint32_t *misc, uint8_t *smem, const
             *reinterpret_cast<uint4 *>(planes + 16u * lane) = make_uint4(bw[0], bw[1], bw[2], bw[3]);
             team_sync<1>();
             uint32_t S[4];
+            if (seg[0] == 8u && seg[1] == 8u) {  // two streams of 8 bytes: 2 x ds_read_b64
+                const uint2 s0 = *reinterpret_cast<const uint2 *>(planes + lane * 8u);
+                const uint2 s1 = *reinterpret_cast<const uint2 *>(planes + 512u + lane * 8u);
+                S[0] = s0.x, S[1] = s0.y, S[2] = s1.x, S[3] = s1.y;
+            } else if (seg[0] == 16u) {  // one stream: ds_read_b128
+                const uint4 s0 = *reinterpret_cast<const uint4 *>(planes + lane * 16u);
+                S[0] = s0.x, S[1] = s0.y, S[2] = s0.z, S[3] = s0.w;
+            } else {
 #pragma unroll
-            for (int d = 0; d < 4; ++d) S[d] = *reinterpret_cast<const uint32_t *>(planes + sd_pb[d] + lane * sd_mul[d]);
+                for (int d = 0; d < 4; ++d)
+                    S[d] = *reinterpret_cast<const uint32_t *>(planes + sd_pb[d] + lane * sd_mul[d]);
+            }
             const uint4 o = make_uint4(perm(S[1], S[0], OA[0]) | perm(S[3], S[2], OB[0]),
                                        perm(S[1], S[0], OA[1]) | perm(S[3], S[2], OB[1]),
                                        perm(S[1], S[0], OA[2]) | perm(S[3], S[2], OB[2]),
