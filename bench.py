@@ -42,8 +42,19 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline duration (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = all usable host cores")
     ap.add_argument("--host-inclusive", action="store_true", help="also time pinned H2D+kernel+D2H")
-    ap.add_argument("--seed", type=int, default=0x5EED0002)
-    return ap.parse_args()
+    ap.add_argument("--seed", type=int, default=None)
+    ap.add_argument("--workload", choices=["c2", "c3", "c4"], default="c3",
+                    help="c3 (default, the BASELINE metric): 262,144 x 64 KiB gradient; c2: 1 Mi x 1 KiB "
+                         "uniform bytes; c4: 4 Mi Zipf(1.5)-sized (64 B - 1 MiB) gradient messages")
+    a = ap.parse_args()
+    if a.workload == "c2":
+        a.msgs = a.msgs if a.msgs != 262144 else 1 << 20
+        a.msg_bytes = 1024 if a.msg_bytes == 65536 else a.msg_bytes
+    if a.workload == "c4" and a.msgs == 262144:
+        a.msgs = 1 << 22
+    if a.seed is None:
+        a.seed = {"c2": 0x5EED0001, "c3": 0x5EED0002, "c4": 0x5EED0003}[a.workload]
+    return a
 
 
 def gen_gradient(torch, n_msgs, msg_bytes, seed, device):
@@ -60,6 +71,28 @@ def gen_gradient(torch, n_msgs, msg_bytes, seed, device):
         x[s:e] = v
         del v, m
     return x.view(torch.uint8)
+
+
+def gen_uniform(torch, nbytes, seed, device):
+    """C2 payloads: uniform random bytes."""
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    return torch.randint(0, 256, (nbytes,), dtype=torch.uint8, device=device, generator=g)
+
+
+def zipf_sizes(n, seed, world=1, rank=0):
+    """C4 message sizes: 64 * r, r ~ Zipf(1.5) on [1, 16384] (64 B - 1 MiB); the whole
+    job's list is drawn once and each rank takes its byte-balanced shard."""
+    import numpy as np
+    from psyne_amd.shard import shard_bounds
+    rng = np.random.default_rng(seed)
+    # truncated Zipf: P(r) ∝ r^-1.5 on [1, 16384] (inverse CDF; mean ≈ 6.3 KB, SURVEY.md §8(d))
+    pmf = np.arange(1, 16385, dtype=np.float64) ** -1.5
+    cdf = np.cumsum(pmf / pmf.sum())
+    r = np.minimum(np.searchsorted(cdf, rng.random(n), side="right") + 1, 16384).astype(np.int64)
+    sizes = 64 * r
+    b = shard_bounds(sizes, world)
+    return sizes[b[rank]:b[rank + 1]]
 
 
 def load_traffic(config_key):
@@ -125,22 +158,39 @@ def main():
 
     from psyne_amd import TDTConfig, TdtCodec
 
+    from psyne_amd.shard import all_true, reduce_max, reduce_sum
     n, mb = a.msgs, a.msg_bytes
-    data = gen_gradient(torch, n, mb, a.seed + rank, dev)
-    off = torch.arange(n + 1, dtype=torch.int64, device=dev) * mb
+    if a.workload == "c4":
+        import numpy as np
+        sizes = zipf_sizes(n * world, a.seed, world, rank)  # the job's list, this rank's shard
+        n = int(sizes.size)
+        offs = np.zeros(n + 1, np.int64)
+        offs[1:] = np.cumsum(sizes)
+        payload = int(offs[-1])
+        data = gen_gradient(torch, 1, payload, a.seed + rank, dev)  # sizes are multiples of 64
+        off = torch.from_numpy(offs).to(dev)
+        cap = int(sum(int(s) for s in (2 * sizes + 28 + 16)))  # Σ tdt_encode_bound (ws 4)
+        hint = 65536
+    else:
+        payload = n * mb
+        data = (gen_uniform(torch, payload, a.seed + rank, dev) if a.workload == "c2"
+                else gen_gradient(torch, n, mb, a.seed + rank, dev))
+        off = torch.arange(n + 1, dtype=torch.int64, device=dev) * mb
+        hint = mb
     codec = TdtCodec(TDTConfig(sample_fraction=1.0), device=local)
     codec.set_metrics(10.0, 1.0, 0.5)  # slow network → compression on (tdt_compression.hpp:200)
-    codec.set_size_hint(mb)
+    codec.set_size_hint(hint)
     # Slotted batches (tdt_encode_batch_into / tdt_decode_batch_into): blob i lands in its own
     # slot of the output buffer, as the reference returns one vector per message; the slot
     # offsets (prefix sums of the encode bounds / of the decoded sizes) are computed on the
     # device inside every step.
-    cap = n * codec.encode_bound(mb)
+    if a.workload != "c4":
+        cap = n * codec.encode_bound(mb)
     enc = torch.empty(cap, dtype=torch.uint8, device=dev)
     eslot = torch.empty(n + 1, dtype=torch.int64, device=dev)
     elen = torch.empty(n, dtype=torch.int64, device=dev)
     est = torch.empty(n, dtype=torch.int32, device=dev)
-    dec = torch.empty(n * mb, dtype=torch.uint8, device=dev)
+    dec = torch.empty(payload, dtype=torch.uint8, device=dev)
     dslot = torch.empty(n + 1, dtype=torch.int64, device=dev)
     dlen = torch.empty(n, dtype=torch.int64, device=dev)
     dst = torch.empty(n, dtype=torch.int32, device=dev)
@@ -182,37 +232,45 @@ def main():
     elapsed = time.perf_counter() - t0
     t_enc = sum(e[0].elapsed_time(e[1]) for e in evs) / a.steps  # ms, encode launch incl. memset
     t_dec = sum(e[1].elapsed_time(e[2]) for e in evs) / a.steps
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        okt = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
-        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
-        ok = bool(okt.item())
+    elapsed = reduce_max(elapsed, dev)  # whole-job time = the slowest rank
+    ok = all_true(ok, dev)
+    job_payload = int(reduce_sum(payload, dev))
 
-    payload = n * mb
     ms_per_step = elapsed / a.steps * 1e3
-    value = world * payload * a.steps / elapsed / 2**30
+    value = job_payload * a.steps / elapsed / 2**30
 
     host = None
-    if a.host_inclusive and rank == 0:
+    if a.host_inclusive and rank == 0 and a.workload != "c4":
         host = host_inclusive(torch, codec, data, off, n, mb)
 
     if rank == 0:
         alg = payload + enc_bytes  # algorithmic bytes per launch (read input once, write output once)
         dom, t_dom = ("tdt_encode_kernel", t_enc) if t_enc >= t_dec else ("tdt_decode_kernel", t_dec)
         achieved = alg / (t_dom * 1e-3) / 1e9
-        key = "c3_%dx%d" % (n, mb)
-        tr = load_traffic(key)
+        key = "%s_%dx%d" % (a.workload, n, mb)
+        tr = load_traffic(key) if a.workload == "c3" else None
         traffic = None
         if tr and dom in tr.get("kernels", {}):
             traffic = tr["kernels"][dom].get("hbm_bytes_per_launch")
         cpu = None
-        if a.cpu_seconds > 0:
+        if a.cpu_seconds > 0 and a.workload == "c3":
             thr = a.cpu_threads or min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "1024")))
             cpu = cpu_baseline(data, mb, a.cpu_seconds, thr)
+        if a.workload == "c3":
+            metric = "TDT encode+decode GiB/s (device-resident), 64 KiB msgs, 1/2/4/8 MI355X"
+            workload = "C3: %d x %d B float32 gradient-like messages per GPU, encode+decode" % (n, mb)
+            data_desc = "synthetic (device-generated gradient-like float32: 70% zeros, N(0,0.01); seed 0x5EED0002+rank)"
+        elif a.workload == "c2":
+            metric = "TDT encode+decode GiB/s (device-resident), 1 KiB uniform msgs"
+            workload = "C2: %d x %d B uniform random messages per GPU, encode+decode" % (n, mb)
+            data_desc = "synthetic (device-generated uniform bytes; seed 0x5EED0001+rank)"
+        else:
+            metric = "TDT encode+decode GiB/s (device-resident), Zipf 64 B-1 MiB mix"
+            workload = ("C4: %d Zipf(1.5)-sized messages (64 B - 1 MiB, %.2f GiB) on this rank of %d, "
+                        "gradient-like content, encode+decode" % (n, payload / 2**30, a.msgs * world))
+            data_desc = "synthetic (device-generated gradient-like float32; sizes seed 0x5EED0003)"
         line = {
-            "metric": "TDT encode+decode GiB/s (device-resident), 64 KiB msgs, 1/2/4/8 MI355X",
+            "metric": metric,
             "value": round(value, 3),
             "unit": "GiB/s",
             "n_gpus": world,
@@ -223,9 +281,9 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic (device-generated gradient-like float32: 70% zeros, N(0,0.01); seed 0x5EED0002+rank)",
-            "config": {"workload": "C3: %d x %d B float32 gradient-like messages per GPU, encode+decode" % (n, mb),
-                       "msgs_per_gpu": n, "msg_bytes": mb, "word_size": 4, "sample_fraction": 1.0,
+            "data": data_desc,
+            "config": {"workload": workload, "msgs_per_gpu": n, "msg_bytes": mb if a.workload != "c4" else None,
+                       "word_size": 4, "sample_fraction": 1.0,
                        "bandwidth_mbps": 10.0, "parallelism": "independent message shards (dp%d)" % world},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),

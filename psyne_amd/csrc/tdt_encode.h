@@ -81,11 +81,13 @@ struct EncLayout {
     static constexpr int W = TEAM / 64;
     static constexpr int WPG = 16 / WS;  // words per 16-byte group
     // histogram, per byte position: [64 per-lane zero bins][256 bins x HC copies] (uint32)
-    static constexpr int HC = 16 / WS;  // 16 KiB of copies whatever the word size
+    // 16 KiB of copies whatever the word size for message-sized teams; one copy for the
+    // one-wave small-message kernel (its LDS footprint sets how many messages a CU holds)
+    static constexpr int HC = TEAM >= 256 ? 16 / WS : 1;
     static constexpr int LOG_HC = HC == 1 ? 0 : HC == 2 ? 1 : HC == 4 ? 2 : HC == 8 ? 3 : 4;
     static constexpr int PS = 64 + 256 * HC;
     static constexpr int HIST = WS * PS * 4;
-    static constexpr int TB = (TEAM >= 256) ? (WS < 4 ? WS : 4) : (WS < 2 ? WS : 2);
+    static constexpr int TB = (TEAM >= 256) ? (WS < 4 ? WS : 4) : 1;
     // one stream's pairs of one wave-round: alignment pad + 1024 pairs + one garbage pair
     static constexpr int WREGION = 16 + 2 * 64 * 16 + 16;
     static constexpr int WSTAGE = 2 * WREGION + 16;  // both streams + a junk pair, per wave
@@ -93,7 +95,8 @@ struct EncLayout {
     static constexpr int TERMS = TB * 256 * 16;
     // Two phases share one region: histogram + entropy terms + log2 tables (dead once the
     // mapping is known) and pass B's per-wave staging windows.
-    static constexpr int ANALYSIS = HIST + TERMS + 2048;
+    // + log2 tables (2 KiB) + the per-message term table for counts 1..64 (1 KiB)
+    static constexpr int ANALYSIS = HIST + TERMS + 2048 + 1024;
     static constexpr int REGION = STAGE > ANALYSIS ? STAGE : ANALYSIS;
     static constexpr int SLOTS = W * 8 * 4;
     static constexpr int MISC = 512;
@@ -101,6 +104,7 @@ struct EncLayout {
     static constexpr int OFF_HIST = 0;
     static constexpr int OFF_TERMS = HIST;
     static constexpr int OFF_LOG2 = HIST + TERMS;
+    static constexpr int OFF_CTAB = HIST + TERMS + 2048;
     static constexpr int OFF_STAGE = 0;
     static constexpr int OFF_SLOTS = REGION;
     static constexpr int OFF_MISC = OFF_SLOTS + SLOTS;
@@ -313,7 +317,7 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
         // float tensors), to this lane's private zero bin — so one ds_add only sends two
         // lanes to the same address when they hold the same nonzero value.
         uint32_t *hist = reinterpret_cast<uint32_t *>(smem + Lay::OFF_HIST);
-        for (int i = tid; i < WS * Lay::PS; i += TEAM) hist[i] = 0;
+        for (int i = tid; i < WS * Lay::PS / 4; i += TEAM) reinterpret_cast<uint4 *>(hist)[i] = make_uint4(0, 0, 0, 0);
         // glibc log2 tables → LDS (the bins' log2 evaluations read them with per-lane indices)
         for (int i = tid; i < 128; i += TEAM) {
             const uint4 v = reinterpret_cast<const uint4 *>(i < 64 ? c_log2_tab : c_log2_tab2)[i & 63];
@@ -358,6 +362,19 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
         double *terms = reinterpret_cast<double *>(smem + Lay::OFF_TERMS);
         const double *ltab = reinterpret_cast<const double *>(smem + Lay::OFF_LOG2);
         const double total = (double)wc;
+        // Counts repeat: the terms of counts 1..64 are computed once per message (exactly the
+        // operations below, so the same bits) and looked up; larger counts are computed.
+        double *ctab = reinterpret_cast<double *>(smem + Lay::OFF_CTAB);
+        if (tid < 64) {
+            double prob;
+            {
+#pragma clang fp contract(off)
+                prob = (double)(uint32_t)(tid + 1) / total;
+                ctab[2 * tid + 1] = psy_log2_glibc(prob, ltab, ltab + 128);
+            }
+            ctab[2 * tid] = -prob;
+        }
+        team_sync<W>();
         for (int q0 = 0; q0 < WS; q0 += Lay::TB) {
             if (q0 > 0) team_sync<W>();  // every wave's chain has read the previous batch
             for (int i = tid; i < Lay::TB * 256; i += TEAM) {
@@ -372,7 +389,7 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
                     if constexpr (MODE == MODE_ANALYZE) {
                         if (a.hist_out) a.hist_out[((uint64_t)msg * WS + b) * 256 + (i & 255)] = c;
                     }
-                    if (c) {
+                    if (c > 64u) {
                         double prob;
                         {
 #pragma clang fp contract(off)
@@ -380,6 +397,10 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
                             L = psy_log2_glibc(prob, ltab, ltab + 128);
                         }
                         np = -prob;
+                    } else if (c) {
+                        const double2 t = reinterpret_cast<const double2 *>(ctab)[c - 1];
+                        np = t.x;
+                        L = t.y;
                     }
                 }
                 terms[2 * i] = np;

@@ -1,0 +1,93 @@
+"""Multi-rank path on CPU: world_size 2 over gloo.
+
+Each rank takes its byte-balanced shard of one batch (psyne_amd.shard), encodes it with the
+CPU oracle (test infrastructure, standing in for the GPU codec), and the gathered shards must
+equal the single-process encoding byte for byte; the bench's max-over-ranks time and
+all-ranks-ok reductions are exercised on the same group."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+import torch.distributed as dist  # noqa: E402
+import torch.multiprocessing as mp  # noqa: E402
+
+from psyne_amd.shard import all_true, reduce_max, shard_bounds, shard_offsets  # noqa: E402
+
+
+def _batch():
+    rng = np.random.default_rng(41)
+    sizes = (64 * np.minimum(rng.zipf(1.5, 300), 256)).astype(np.int64)
+    msgs = []
+    for i, n in enumerate(sizes):
+        x = rng.normal(0, 0.01, int(n) // 4).astype(np.float32)
+        x[rng.random(x.size) < 0.7] = 0
+        msgs.append(x.view(np.uint8) if i % 3 else rng.integers(0, 256, int(n), dtype=np.uint8))
+    off = np.zeros(len(msgs) + 1, np.int64)
+    off[1:] = np.cumsum([m.size for m in msgs])
+    return msgs, off
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle.oracle import Oracle
+        orc = Oracle()
+        msgs, off = _batch()
+        b = shard_bounds(np.diff(off), world)
+        mine = [orc.encode(m, bandwidth=10.0) for m in msgs[b[rank]:b[rank + 1]]]
+        local_off = shard_offsets(off, b, rank)
+        assert local_off[0] == 0 and local_off[-1] == off[b[rank + 1]] - off[b[rank]]
+        gathered = [None] * world
+        dist.all_gather_object(gathered, mine)
+        t = reduce_max(float(rank + 1))
+        ok = all_true(rank == 0)  # rank 1 says False → AND is False
+        if rank == 0:
+            q.put((gathered, t, ok, b.tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_shard_bounds_balanced():
+    sizes = np.array([100, 1, 1, 1, 1, 1, 100, 1, 1000, 1], np.int64)
+    for world in (1, 2, 3, 4, 8):
+        b = shard_bounds(sizes, world)
+        assert b[0] == 0 and b[-1] == sizes.size and np.all(np.diff(b) >= 0)
+        per = [int(sizes[b[r]:b[r + 1]].sum()) for r in range(world)]
+        assert sum(per) == sizes.sum()
+        assert max(per) - min(per) <= sizes.max() + sizes.sum() // world
+    assert shard_bounds(np.zeros(5, np.int64), 2).tolist() == [0, 2, 5]
+
+
+def test_two_rank_gloo_shards_match_single_process():
+    from oracle.oracle import Oracle
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    gathered, t, ok, bounds = q.get(timeout=180)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert t == 2.0 and ok is False
+    msgs, off = _batch()
+    orc = Oracle()
+    single = [orc.encode(m, bandwidth=10.0) for m in msgs]
+    flat = [blob for shard in gathered for blob in shard]
+    assert flat == single
+    assert bounds[0] == 0 and bounds[-1] == len(msgs) and 0 < bounds[1] < len(msgs)
