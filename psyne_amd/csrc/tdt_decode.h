@@ -187,6 +187,7 @@ __device__ __forceinline__ void decode_fast(uint32_t *misc, uint8_t *smem, const
     using Lay = DecLayout;
     constexpr uint32_t WR = kFastWR;
     const uint32_t lane = (uint32_t)lane_id();
+    PSY_PROF_BEGIN();
     uint16_t *heads = reinterpret_cast<uint16_t *>(smem + Lay::OFF_HEADS);
     uint8_t *planes = smem + Lay::OFF_PLANES;
     const bool two = nref == 2;
@@ -298,6 +299,7 @@ __device__ __forceinline__ void decode_fast(uint32_t *misc, uint8_t *smem, const
             }
         }
         team_sync<1>();
+        PSY_PROF_MARK(9);
         // ---- per round: fill, recombine, store
         for (uint32_t rl = 0; rl < WR; ++rl) {
             const uint32_t g0 = gwin + rl * 64u;
@@ -367,6 +369,7 @@ __device__ __forceinline__ void decode_fast(uint32_t *misc, uint8_t *smem, const
             }
             team_sync<1>();  // planes are rewritten by the next round
         }
+        PSY_PROF_MARK(10);
     }
 }
 

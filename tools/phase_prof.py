@@ -24,11 +24,12 @@ DEC = {8: "header+look-back", 9: "pair rounds", 10: "fill+scatter", 11: "store"}
 def build():
     from psyne_amd import build as b
     cmd = [b.HIPCC, f"--offload-arch={b.ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-DPSY_PROF=1",
+           "-DPSY_FAST_BUILD",
            "-I", str(ROOT / "include"), *map(str, b.SOURCES), "-o", str(PROF_LIB)]
     subprocess.check_call(cmd)
 
 
-def run(msgs, msg_bytes, seed):
+def run(msgs, msg_bytes, seed, uniform=False):
     import torch
     from psyne_amd import _lib
     from psyne_amd.tdt import TdtCodec, TDTConfig
@@ -38,8 +39,10 @@ def run(msgs, msg_bytes, seed):
     lib.tdt_prof_read.restype = C.c_int
     codec = TdtCodec(TDTConfig(sample_fraction=1.0), lib=lib)
     codec.set_metrics(10.0, 1.0, 0.5)
+    codec.set_size_hint(msg_bytes)
     dev = torch.device("cuda:0")
-    data = bench.gen_gradient(torch, msgs, msg_bytes, seed, dev)
+    data = (bench.gen_uniform(torch, msgs * msg_bytes, seed, dev) if uniform
+            else bench.gen_gradient(torch, msgs, msg_bytes, seed, dev))
     off = torch.arange(msgs + 1, dtype=torch.int64, device=dev) * msg_bytes
     buf = (C.c_uint64 * 32)()
     for it in range(3):
@@ -70,8 +73,9 @@ if __name__ == "__main__":
     ap.add_argument("--msgs", type=int, default=32768)
     ap.add_argument("--msg-bytes", type=int, default=65536)
     ap.add_argument("--seed", type=int, default=0x5EED0002)
+    ap.add_argument("--uniform", action="store_true")
     a = ap.parse_args()
     if a.build:
         build()
     else:
-        run(a.msgs, a.msg_bytes, a.seed)
+        run(a.msgs, a.msg_bytes, a.seed, a.uniform)
