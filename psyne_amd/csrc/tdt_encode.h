@@ -746,6 +746,7 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
             }
         }
 
+#ifdef PSY_EMIT_V4
         // Emit the pairs of round r: Tw its slot word, C its chunk-start mask, nxt63 the chunk
         // bits of the group after lane 63's (combined layout).
         auto emit = [&](uint32_t r, const uint4 &Tw, uint32_t C, uint32_t nxt63) __attribute__((always_inline)) {
@@ -878,14 +879,114 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
             }
             team_sync<1>();  // the window is rewritten by the next round
         };
+#endif
+
+#ifndef PSY_EMIT_V4
+        // ---------------------------------------------------------------- emit v5
+        // Chunk-START entries: every chunk start writes entry = value << 24 | (position within
+        // the round + 256) at its rank among the round's starts (slot 0 of each stream holds
+        // the chunk still open from the previous round / wave); the flush then forms pair k
+        // from entries k and k+1 — count = their position difference (<= 255 by the cap),
+        // value = entry k's — one pair per lane, 2-byte stores coalesced across the wave.  The
+        // last chunk of a round stays pending; the stream's final chunk ends at its length.
+        uint32_t pi5[2] = {0, 0}, pend[2] = {0, 0};
+        bool hp[2] = {false, false};
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            if (c == 1 && !ns2) break;
+            const uint32_t p_in = __builtin_amdgcn_readfirstlane(pin[c]);
+            if (p_in > 0 && ccarry[c] > 0) {
+                hp[c] = true;
+                pi5[c] = p_in - 1;
+                const uint32_t val = (edc0 >> (8 * c)) & 0xffu;  // the chunk's value: the byte before the wave
+                pend[c] = (val << 24) | (ccarry[c] - 1u + 256u - gw0 * Ls[c]);
+            }
+        }
+        const uint32_t slen[2] = {wc * k0, wc * k1};
+        const uint32_t eoff1 = 4u * (1u + 64u * L0);  // stream 1's entry region (bytes)
+        const uint32_t junk = wst + 4u * (2u + 64u * 16u);
+        const uint32_t pb0 = (uint32_t)lane * Ls[0] + 256u, pb1 = (uint32_t)lane * Ls[1] + 256u - L0;
+        auto emit5 = [&](uint32_t r, const uint4 &Tw, uint32_t C) __attribute__((always_inline)) {
+            PSY_ASM_ROUND(B);
+            const uint32_t T[4] = {Tw.x, Tw.y, Tw.z, Tw.w};
+            const uint32_t gr = gw0 + r * 64;
+            const uint32_t c0 = popc(C & lowL0);
+            const uint32_t pc = c0 | (popc(C >> L0) << 16);
+            const uint32_t pinc = wave_incl_scan<OpAdd>(pc);
+            const uint32_t pexc = pinc - pc;
+            const uint32_t Stot = rdlane(pinc, 63);
+            const uint32_t S[2] = {Stot & 0xffffu, Stot >> 16};
+            const uint32_t eb0 = wst + 4u * (1u + (pexc & 0xffffu));
+            const uint32_t eb1 = wst + eoff1 + 4u * (1u + (pexc >> 16) - c0);
+            if (lane == 0) {
+                if (hp[0]) *reinterpret_cast<uint32_t *>(smem + wst) = pend[0];
+                if (ns2 && hp[1]) *reinterpret_cast<uint32_t *>(smem + wst + eoff1) = pend[1];
+            }
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const int q = j & 3, t = j >> 2;
+                const bool s0 = (uint32_t)j < L0;
+                const uint32_t ad = (s0 ? eb0 : eb1) + 4u * popc(C & ((1u << j) - 1u));
+                const uint32_t a2 = ((C >> j) & 1u) ? ad : junk;
+                const uint32_t pos = (s0 ? pb0 : pb1) + (uint32_t)j;
+                *reinterpret_cast<uint32_t *>(smem + a2) =
+                    perm(T[q], pos, ((uint32_t)(4 + t) << 24) | 0x000c0100u);
+            }
+            team_sync<1>();
+            const bool last = gr <= ngroups - 1 && ngroups - 1 < gr + 64;  // the stream's end is here
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                if (c == 1 && !ns2) break;
+                const uint32_t f0 = hp[c] ? 0u : 1u;
+                const uint32_t nent = S[c] + (hp[c] ? 1u : 0u);
+                const uint32_t K = nent ? nent - 1u : 0u;
+                const uint32_t eb = wst + (c ? eoff1 : 0u);
+                uint8_t *const D = dst + sdata[c] + 2ull * pi5[c];
+                const bool even = ((uintptr_t)D & 1) == 0;
+                for (uint32_t k0 = 0; k0 < K; k0 += 64) {
+                    const uint32_t k = k0 + (uint32_t)lane;
+                    if (k < K) {
+                        const uint32_t e0 = *reinterpret_cast<const uint32_t *>(smem + eb + 4u * (f0 + k));
+                        const uint32_t e1 = *reinterpret_cast<const uint32_t *>(smem + eb + 4u * (f0 + k + 1u));
+                        const uint32_t pair = perm(e0, e1 - e0, 0x0c0c0700u);  // count, value
+                        if (even) {
+                            *reinterpret_cast<uint16_t *>(D + 2u * k) = (uint16_t)pair;
+                        } else {
+                            D[2u * k] = (uint8_t)pair;
+                            D[2u * k + 1u] = (uint8_t)(pair >> 8);
+                        }
+                    }
+                }
+                pi5[c] += K;
+                if (nent) {
+                    const uint32_t el = __builtin_amdgcn_readfirstlane(*reinterpret_cast<const uint32_t *>(smem + eb + 4u * S[c]));
+                    if (last) {  // the final chunk runs to the end of the stream
+                        if (lane == 0) {
+                            const uint32_t cnt = slen[c] - (gr * Ls[c] + (el & 0xffffu) - 256u);
+                            D[2u * K] = (uint8_t)cnt;
+                            D[2u * K + 1u] = (uint8_t)(el >> 24);
+                        }
+                        pi5[c] += 1;
+                    }
+                    pend[c] = el - 64u * Ls[c];  // rebased to the next round
+                    hp[c] = true;
+                }
+            }
+            team_sync<1>();  // the entries are rewritten by the next round
+        };
+#endif
 
         if (resident) {
 #pragma unroll
             for (int r = 0; r < G; ++r) {
                 if ((uint32_t)r < RW) {
+#ifndef PSY_EMIT_V4
+                    emit5((uint32_t)r, dres[r], cres[r]);
+#else
                     uint32_t nx = nfb;
                     if (r + 1 < G && (uint32_t)(r + 1) < RW) nx = rdlane(cres[r + 1 < G ? r + 1 : r], 0);
                     emit((uint32_t)r, dres[r], cres[r], nx);
+#endif
                 }
             }
         } else {
@@ -909,7 +1010,11 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
                 uint4 Tn = make_uint4(0, 0, 0, 0);
                 uint32_t Cn = 0;
                 if (r + 1 < RW) Cn = chunk_of(r + 1, load_group(gw0 + (r + 1) * 64 + lane), Tn);
+#ifndef PSY_EMIT_V4
+                emit5(r, Tc, Cc);
+#else
                 emit(r, Tc, Cc, r + 1 < RW ? rdlane(Cn, 0) : nfb);
+#endif
                 Tc = Tn;
                 Cc = Cn;
             }
