@@ -264,20 +264,27 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
         return 16ull * (gw0 + r * 64 + 64) <= n;
     };
 
-    // Resident messages keep their RW <= G rounds in VGPRs.  The round loop ROTATES the
-    // arrays (compile-time indices only) instead of indexing them with the round number,
-    // which would push them to scratch.
-    uint4 dres[G];     // the round's 16 bytes per lane; after pass A1 its slot word T
-    uint32_t cres[G];  // run-start masks (A1 → A2), then chunk-start masks (A2 → B)
+    // The rest of the kernel is instantiated twice: RES (the message's RW <= G rounds stay in
+    // VGPRs) and streaming (every pass re-reads its rounds from HBM).  Two separate code paths,
+    // so the register allocator never has to keep the resident arrays alive across the
+    // streaming loops (which spilled them to scratch when both shared one path).
+    auto run = [&](auto res_tag) __attribute__((always_inline)) {
+    constexpr bool RES = decltype(res_tag)::value;
+    constexpr int GR = RES ? G : 1;
+    // Resident rounds live in fully unrolled loops (compile-time indices only): indexing the
+    // arrays with a run-time round number would push them to scratch.
+    uint4 dres[GR];     // the round's 16 bytes per lane; after pass A1 its slot word T
+    uint32_t cres[GR];  // run-start masks (A1 → A2), then chunk-start masks (A2 → B)
+    if constexpr (RES) {
 #pragma unroll
-    for (int r = 0; r < G; ++r) {
-        dres[r] = (resident && (uint32_t)r < RW) ? load_group(gw0 + r * 64 + lane) : make_uint4(0, 0, 0, 0);
-        cres[r] = 0;
+        for (int r = 0; r < G; ++r) {
+            dres[r] = ((uint32_t)r < RW) ? load_group(gw0 + r * 64 + lane) : make_uint4(0, 0, 0, 0);
+            cres[r] = 0;
+        }
     }
-    // body(r, data&, cres&, resident) for every round r < RW of this wave, in order.  Resident
-    // rounds: unrolled, compile-time indices; otherwise the round is loaded from HBM.
+    // body(r, data&, cres&, res) for every round r < RW of this wave, in order.
     auto for_rounds = [&](auto &&body) __attribute__((always_inline)) {
-        if (resident) {
+        if constexpr (RES) {
 #pragma unroll
             for (int r = 0; r < G; ++r)
                 if ((uint32_t)r < RW) body((uint32_t)r, dres[r], cres[r], std::true_type{});
@@ -976,7 +983,7 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
         };
 #endif
 
-        if (resident) {
+        if constexpr (RES) {
 #pragma unroll
             for (int r = 0; r < G; ++r) {
                 if ((uint32_t)r < RW) {
@@ -1021,6 +1028,9 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
         }
         PSY_PROF_MARK(6);
     }
+    };  // run
+    if (resident) run(std::true_type{});
+    else run(std::false_type{});
 }
 
 }  // namespace psy
