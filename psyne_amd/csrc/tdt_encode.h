@@ -90,7 +90,11 @@ struct EncLayout {
     static constexpr int TB = (TEAM >= 256) ? (WS < 4 ? WS : 4) : 1;
     // one stream's pairs of one wave-round: alignment pad + 1024 pairs + one garbage pair
     static constexpr int WREGION = 16 + 2 * 64 * 16 + 16;
-    static constexpr int WSTAGE = 2 * WREGION + 16;  // both streams + a junk pair, per wave
+    // per wave: v4 emit — both streams' pair windows + a junk pair; v5 emit — 64 junk dwords,
+    // then (pending + up to 64·16 entries) for the two streams together
+    static constexpr int WSTAGE_V4 = 2 * WREGION + 16;
+    static constexpr int WSTAGE_V5 = 256 + 4 * (2 + 64 * 16);
+    static constexpr int WSTAGE = ((WSTAGE_V4 > WSTAGE_V5 ? WSTAGE_V4 : WSTAGE_V5) + 15) / 16 * 16;
     static constexpr int STAGE = W * WSTAGE;
     static constexpr int TERMS = TB * 256 * 16;
     // Two phases share one region: histogram + entropy terms + log2 tables (dead once the
@@ -161,7 +165,9 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
     uint32_t *misc = reinterpret_cast<uint32_t *>(smem + Lay::OFF_MISC);
     const int tid = threadIdx.x;
     const int lane = lane_id();
-    const int wv = tid >> 6;
+    // wave index, made provably uniform: everything derived from it (group ranges, round
+    // bounds, full-round tests) is then scalar code instead of per-lane VALU work
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     PSY_PROF_BEGIN();
 
     // Message id: the look-back needs ids in dispatch order (atomic ticket); slotted outputs
@@ -910,10 +916,16 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
             }
         }
         const uint32_t slen[2] = {wc * k0, wc * k1};
+        // per wave: 64 junk dwords (one per lane), then stream 0's pending entry + entries,
+        // then stream 1's (EncLayout::WSTAGE)
+        const uint32_t ebase = wst + 256u;
+        const uint32_t jl = wst + 4u * (uint32_t)lane;
         const uint32_t eoff1 = 4u * (1u + 64u * L0);  // stream 1's entry region (bytes)
-        const uint32_t junk = wst + 4u * (2u + 64u * 16u);
         const uint32_t pb0 = (uint32_t)lane * Ls[0] + 256u, pb1 = (uint32_t)lane * Ls[1] + 256u - L0;
         auto emit5 = [&](uint32_t r, const uint4 &Tw, uint32_t C) __attribute__((always_inline)) {
+#ifdef PSY_X_NOEMIT
+            if (r < 100) return;
+#endif
             PSY_ASM_ROUND(B);
             const uint32_t T[4] = {Tw.x, Tw.y, Tw.z, Tw.w};
             const uint32_t gr = gw0 + r * 64;
@@ -923,21 +935,27 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
             const uint32_t pexc = pinc - pc;
             const uint32_t Stot = rdlane(pinc, 63);
             const uint32_t S[2] = {Stot & 0xffffu, Stot >> 16};
-            const uint32_t eb0 = wst + 4u * (1u + (pexc & 0xffffu));
-            const uint32_t eb1 = wst + eoff1 + 4u * (1u + (pexc >> 16) - c0);
             if (lane == 0) {
-                if (hp[0]) *reinterpret_cast<uint32_t *>(smem + wst) = pend[0];
-                if (ns2 && hp[1]) *reinterpret_cast<uint32_t *>(smem + wst + eoff1) = pend[1];
+                if (hp[0]) *reinterpret_cast<uint32_t *>(smem + ebase) = pend[0];
+                if (ns2 && hp[1]) *reinterpret_cast<uint32_t *>(smem + ebase + eoff1) = pend[1];
             }
+            // D = (address of this lane's next entry in the current stream) - its junk dword.
+            // Slot j writes at jl + bit_j·D (a start: its entry; otherwise the junk dword),
+            // then D advances by one entry on a start: 4 VALU per slot, no compares.
+            const uint32_t D0 = ebase + 4u * (1u + (pexc & 0xffffu)) - jl;
+            const uint32_t D1 = ebase + eoff1 + 4u * (1u + (pexc >> 16)) - jl;
+            uint32_t D = L0 == 0 ? D1 : D0;
 #pragma unroll
             for (int j = 0; j < 16; ++j) {
                 const int q = j & 3, t = j >> 2;
+                if (j > 0 && j % WPG == 0 && (uint32_t)j == L0) D = D1;  // stream 1 begins (uniform)
                 const bool s0 = (uint32_t)j < L0;
-                const uint32_t ad = (s0 ? eb0 : eb1) + 4u * popc(C & ((1u << j) - 1u));
-                const uint32_t a2 = ((C >> j) & 1u) ? ad : junk;
+                const uint32_t bit = (C >> j) & 1u;
+                const uint32_t ad = (uint32_t)__umul24(bit, D) + jl;
                 const uint32_t pos = (s0 ? pb0 : pb1) + (uint32_t)j;
-                *reinterpret_cast<uint32_t *>(smem + a2) =
+                *reinterpret_cast<uint32_t *>(smem + ad) =
                     perm(T[q], pos, ((uint32_t)(4 + t) << 24) | 0x000c0100u);
+                D += bit << 2;
             }
             team_sync<1>();
             const bool last = gr <= ngroups - 1 && ngroups - 1 < gr + 64;  // the stream's end is here
@@ -947,7 +965,7 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
                 const uint32_t f0 = hp[c] ? 0u : 1u;
                 const uint32_t nent = S[c] + (hp[c] ? 1u : 0u);
                 const uint32_t K = nent ? nent - 1u : 0u;
-                const uint32_t eb = wst + (c ? eoff1 : 0u);
+                const uint32_t eb = ebase + (c ? eoff1 : 0u);
                 uint8_t *const D = dst + sdata[c] + 2ull * pi5[c];
                 const bool even = ((uintptr_t)D & 1) == 0;
                 for (uint32_t k0 = 0; k0 < K; k0 += 64) {
