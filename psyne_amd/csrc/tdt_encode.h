@@ -967,6 +967,52 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
                 const uint32_t K = nent ? nent - 1u : 0u;
                 const uint32_t eb = ebase + (c ? eoff1 : 0u);
                 uint8_t *const D = dst + sdata[c] + 2ull * pi5[c];
+#ifdef PSY_FLUSH_WIN
+                // (diagnostic variant, measured slower: 15.9 vs 14.5 ms — the extra LDS round trip
+                // costs more than the 2-byte stores it saves)
+                // Pairs go to an LDS window congruent (mod 16) with D — pair k at byte
+                // wst + (D mod 16) + 2k, always below the entries still to be read — and leave
+                // in 16-byte stores (a 2-byte store per pair costs the vector memory path 8x
+                // the instructions).  The final chunk of the stream, when it ends here, is one
+                // more pair: count = stream length - its start.
+                if (nent) {
+                    const uint32_t el = __builtin_amdgcn_readfirstlane(*reinterpret_cast<const uint32_t *>(smem + eb + 4u * S[c]));
+                    const uint32_t Kw = K + (last ? 1u : 0u);
+                    const uint32_t ra = (uint32_t)((uintptr_t)D & 15);
+                    const uint32_t wb = wst + ra;
+                    const uint32_t fin = ((slen[c] - (gr * Ls[c] + (el & 0xffffu) - 256u)) & 0xffu) | ((el >> 24) << 8);
+                    for (uint32_t k0 = 0; k0 < Kw; k0 += 64) {
+                        const uint32_t k = k0 + (uint32_t)lane;
+                        if (k < Kw) {
+                            const uint32_t e0 = *reinterpret_cast<const uint32_t *>(smem + eb + 4u * (f0 + k));
+                            const uint32_t e1 = *reinterpret_cast<const uint32_t *>(smem + eb + 4u * (f0 + k + 1u));
+                            const uint32_t pair = k < K ? perm(e0, e1 - e0, 0x0c0c0700u) : fin;  // count, value
+                            *reinterpret_cast<uint16_t *>(smem + wb + 2u * k) = (uint16_t)pair;
+                        }
+                    }
+                    team_sync<1>();
+                    // head and tail bytes in ONE byte-store instruction (lanes 0-15 head, lanes
+                    // 32-47 tail), the body as aligned 16-byte stores (at most 2 per lane)
+                    const uint32_t len = 2u * Kw;
+                    const uint32_t head0 = (16u - ra) & 15u;
+                    const uint32_t head = head0 < len ? head0 : len;
+                    const uint32_t body16 = (len - head) >> 4;
+                    const uint32_t tail = len - head - 16u * body16;
+                    const uint32_t ht = (uint32_t)lane < 16u ? (uint32_t)lane : head + 16u * body16 + ((uint32_t)lane - 32u);
+                    if ((uint32_t)lane < head || ((uint32_t)lane - 32u) < tail) D[ht] = smem[wb + ht];
+#pragma unroll
+                    for (uint32_t it = 0; it < 2; ++it) {
+                        const uint32_t k = (uint32_t)lane + 64u * it;
+                        if (k < body16)
+                            *reinterpret_cast<uint4 *>(D + head + 16u * k) =
+                                *reinterpret_cast<const uint4 *>(smem + wb + head + 16u * k);
+                    }
+                    pi5[c] += Kw;
+                    pend[c] = el - 64u * Ls[c];  // rebased to the next round
+                    hp[c] = true;
+                    team_sync<1>();  // the window is rewritten by the next stream
+                }
+#else
                 const bool even = ((uintptr_t)D & 1) == 0;
                 for (uint32_t k0 = 0; k0 < K; k0 += 64) {
                     const uint32_t k = k0 + (uint32_t)lane;
@@ -996,6 +1042,7 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
                     pend[c] = el - 64u * Ls[c];  // rebased to the next round
                     hp[c] = true;
                 }
+#endif
             }
             team_sync<1>();  // the entries are rewritten by the next round
         };
