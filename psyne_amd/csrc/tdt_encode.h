@@ -625,7 +625,24 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
         if (gw0 > 0 && gw0 - 1 < ngroups) edc0 = __builtin_amdgcn_readfirstlane(edges(load_group(gw0 - 1)));
 
         // ---------------------------------------------------------- pass A1: run starts
+        // A1 also proves, for nearly every message, that the 255-cap cannot occur, so that
+        // A2's scan is skipped.  A cap needs a run of >= 256 bytes, i.e. at least
+        // Zr = floor(255 / Ls) - 1 consecutive groups without a run start in that stream, and
+        // any 2B - 1 consecutive groups contain a B-aligned block of B groups (B divides 64, so
+        // rounds and waves start on block boundaries).  With B = 8 for Ls < 16 (Zr >= 16) and
+        // B = 4 for Ls = 16 (Zr = 14), "every aligned B-group block holds a start (or reaches
+        // past the end)" rules the cap out.  Per round and stream: one ballot and a
+        // has-zero-byte (B = 8) or has-zero-nibble (B = 4) test on it, on the scalar unit
+        // (tests/test_cap_exclusion.py checks the rule against adversarial run lengths).
         uint32_t wmax[2] = {0, 0};
+        uint64_t zk1[2], zk8[2];
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            const bool b8 = Ls[c] < 16u;
+            zk1[c] = b8 ? 0x0101010101010101ull : 0x1111111111111111ull;
+            zk8[c] = Ls[c] == 0u ? 0ull : b8 ? 0x8080808080808080ull : 0x8888888888888888ull;
+        }
+        uint64_t zacc = 0;
         {
             uint32_t edc = edc0;
             for_rounds([&](uint32_t r, uint4 &d, uint32_t &cm, auto res) __attribute__((always_inline)) {
@@ -641,9 +658,14 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
                 if constexpr (decltype(res)::value) d = make_uint4(T[0], T[1], T[2], T[3]);
                 const uint32_t m0 = m & lowL0;
                 if (m0) wmax[0] = umax(wmax[0], g * Ls[0] + hibit(m0) + 1u);
+                const uint64_t pastm = full_round(r) ? 0ull : (uint64_t)__ballot(g >= ngroups);
+                const uint64_t b0 = (uint64_t)__ballot(m0 != 0u) | pastm;
+                zacc |= (b0 - zk1[0]) & ~b0 & zk8[0];
                 if (ns2) {
                     const uint32_t m1 = m >> L0;
                     if (m1) wmax[1] = umax(wmax[1], g * Ls[1] + hibit(m1) + 1u);
+                    const uint64_t b1 = (uint64_t)__ballot(m1 != 0u) | pastm;
+                    zacc |= (b1 - zk1[1]) & ~b1 & zk8[1];
                 }
             });
         }
@@ -652,17 +674,22 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
         if (lane == 0) {
             slots[wv * 8 + 0] = wmax[0];
             slots[wv * 8 + 1] = wmax[1];
+            slots[wv * 8 + 5] = zacc != 0ull ? 1u : 0u;
         }
         team_sync<W>();
         uint32_t rin[2] = {0, 0};  // max (run start + 1) before this wave
+        uint32_t capped = 0;       // some wave cannot rule the 255-cap out
 #pragma unroll
-        for (int ww = 0; ww < W; ++ww)
+        for (int ww = 0; ww < W; ++ww) {
             if (ww < wv) {
                 rin[0] = umax(rin[0], slots[ww * 8 + 0]);
                 rin[1] = umax(rin[1], slots[ww * 8 + 1]);
             }
+            capped |= slots[ww * 8 + 5];
+        }
         rin[0] = __builtin_amdgcn_readfirstlane(rin[0]);
         rin[1] = __builtin_amdgcn_readfirstlane(rin[1]);
+        const bool clean = __builtin_amdgcn_readfirstlane(capped) == 0u;
         PSY_PROF_MARK(3);
 
         // ---------------------------------------------------------- pass A2: chunk starts
@@ -685,7 +712,7 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
                     m = run_mask(T, ed, edc, g, V);
                     edc = rdlane(ed, 63);
                 }
-                const uint32_t C = chunk_round(r, m, rcarry, g, V);
+                const uint32_t C = clean ? m : chunk_round(r, m, rcarry, g, V);
                 cm = C;
                 pc0 += popc(C & lowL0);
                 pc1 += popc(C >> L0);
@@ -1074,7 +1101,7 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
                 const uint32_t ed = edges(d);
                 const uint32_t m = run_mask(T, ed, edc, g, V);
                 edc = rdlane(ed, 63);
-                return chunk_round(r, m, rcarry, g, V);
+                return clean ? m : chunk_round(r, m, rcarry, g, V);
             };
             uint4 Tc;
             uint32_t Cc = chunk_of(0, load_group(gw0 + lane), Tc);

@@ -227,6 +227,23 @@ def test_rle_cap_boundaries(orc):
     check_vs_oracle(orc, make_codec(hint=1024), msgs)
 
 
+def test_cap_exclusion_near_threshold(orc):
+    """64 KiB messages (8-wave resident kernel) with word-level runs of 110-140 words (~256
+    stream bytes per 2-byte stream, 30-34 groups): the pass-A1 block test must send every
+    message that can hit the 255-cap through pass A2 (tests/test_cap_exclusion.py)."""
+    rng = np.random.default_rng(18)
+    msgs = []
+    for t in range(24):
+        x = grad(rng, 16384).view(np.uint32).copy()
+        for _ in range(1 + t % 3):
+            L = int(rng.integers(110, 141))
+            at = int(rng.integers(0, 16384 - L))
+            x[at:at + L] = 0 if t % 2 else x[at]
+        msgs.append(x.view(np.uint8))
+    check_vs_oracle(orc, make_codec(), msgs)
+    check_vs_oracle(orc, make_codec(hint=1024), msgs[:6])
+
+
 @pytest.mark.parametrize("ws", [1, 2, 8, 16])
 def test_word_sizes(orc, ws):
     rng = np.random.default_rng(17 + ws)
