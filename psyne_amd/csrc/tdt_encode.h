@@ -251,8 +251,10 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
     const uint32_t wc = n32 / WS;
     const uint32_t ngroups = (n32 + 15) / 16;
     const uint32_t RW = (ngroups + TEAM - 1) / TEAM;  // rounds per wave
-    const bool resident = RW <= (uint32_t)G;
     const bool al16 = ((uintptr_t)base & 15) == 0;
+    // Resident: the rounds fit in VGPRs and every group is a whole aligned 16 bytes, so the
+    // loads are straight-line dwordx4s (below); anything else streams.
+    const bool resident = RW <= (uint32_t)G && al16 && (n32 & 15u) == 0;
     const uint32_t gw0 = (uint32_t)wv * RW * 64;  // first group of this wave
 
     auto vbytes = [&](uint32_t g) __attribute__((always_inline)) -> uint32_t {
@@ -281,10 +283,27 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
     // arrays with a run-time round number would push them to scratch.
     uint4 dres[GR];     // the round's 16 bytes per lane; after pass A1 its slot word T
     uint32_t cres[GR];  // run-start masks (A1 → A2), then chunk-start masks (A2 → B)
+    // glibc log2 tables for the entropy pass, fetched BEFORE the message's rounds so that the
+    // LDS copy below waits for these loads only (issued after the rounds, its wait would
+    // cover every round's load and stall the team until the whole message had arrived)
+    constexpr int NL2 = (128 + TEAM - 1) / TEAM;
+    uint4 l2v[NL2];
+    if constexpr (MODE != MODE_MAPPED) {
+#pragma unroll
+        for (int k = 0; k < NL2; ++k) {
+            const int i = (tid + k * TEAM) & 127;
+            l2v[k] = reinterpret_cast<const uint4 *>(i < 64 ? c_log2_tab : c_log2_tab2)[i & 63];
+        }
+    }
     if constexpr (RES) {
+        // One unconditional dwordx4 per lane and round, all in flight before the first use (a
+        // branchy load per round made the compiler wait for each before issuing the next).
+        // Lanes past the end load the message's first group instead; every pass masks them by
+        // vbytes / vmask.
 #pragma unroll
         for (int r = 0; r < G; ++r) {
-            dres[r] = ((uint32_t)r < RW) ? load_group(gw0 + r * 64 + lane) : make_uint4(0, 0, 0, 0);
+            const uint32_t g = gw0 + r * 64 + lane;
+            dres[r] = *reinterpret_cast<const uint4 *>(base + 16ull * (g < ngroups ? g : 0u));
             cres[r] = 0;
         }
     }
@@ -332,10 +351,9 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
         uint32_t *hist = reinterpret_cast<uint32_t *>(smem + Lay::OFF_HIST);
         for (int i = tid; i < WS * Lay::PS / 4; i += TEAM) reinterpret_cast<uint4 *>(hist)[i] = make_uint4(0, 0, 0, 0);
         // glibc log2 tables → LDS (the bins' log2 evaluations read them with per-lane indices)
-        for (int i = tid; i < 128; i += TEAM) {
-            const uint4 v = reinterpret_cast<const uint4 *>(i < 64 ? c_log2_tab : c_log2_tab2)[i & 63];
-            reinterpret_cast<uint4 *>(smem + Lay::OFF_LOG2)[i] = v;
-        }
+#pragma unroll
+        for (int k = 0; k < NL2; ++k)
+            if (tid + k * TEAM < 128) reinterpret_cast<uint4 *>(smem + Lay::OFF_LOG2)[tid + k * TEAM] = l2v[k];
         team_sync<W>();
         const uint32_t zoff = (uint32_t)lane * 4u;
         const uint32_t coff = (64u + ((uint32_t)lane & (Lay::HC - 1))) * 4u;
