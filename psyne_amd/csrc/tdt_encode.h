@@ -11,12 +11,13 @@
 //   simple_rle_compress    :557-582  (count <= 255, value) pairs
 //   TDTEncodedData::serialize :81-117
 //
-// Work decomposition: one TEAM-thread workgroup per message, message ids
-// claimed through an atomic ticket.  A message is a sequence of 16-byte GROUPS.  Wave w owns
-// the contiguous group range [w·RW·64, (w+1)·RW·64); round r of the wave is one coalesced
-// 1 KiB sweep (lane l ↔ group (w·RW + r)·64 + l).  Messages of up to G rounds per wave stay
-// in VGPRs across all passes: the resident round loops are fully unrolled (compile-time
-// array indices, no register moves); pass A1 replaces each round's bytes by its slot word T.
+// Work decomposition: one TEAM-thread workgroup per message (message id =
+// blockIdx for slotted outputs, an atomic ticket for the compacted look-back API).  A message
+// is a sequence of 16-byte GROUPS.  Wave w owns the contiguous group range [w·RW·64,
+// (w+1)·RW·64); round r of the wave is one coalesced 1 KiB sweep (lane l ↔ group
+// (w·RW + r)·64 + l).  Aligned whole-group messages of up to G rounds per wave stay in VGPRs
+// across all passes (a separate instantiation of the kernel body: fully unrolled round loops,
+// compile-time array indices); pass A1 replaces each round's bytes by its slot word T.
 //
 // Both streams of a group live in ONE 16-slot word — stream 0 in slots [0, L0), stream 1 in
 // [L0, 16) — transposed so that slot j = 4t + q is byte t of dword q: the byte before slot j
@@ -25,15 +26,16 @@
 // scan (two u16 halves: v_pk_max_u16 / carry-free adds).  Passes per message:
 //   H   histograms into replicated LDS bins (+ per-lane zero bins: no same-address atomics)
 //   E   entropies (exact fma chain) → mapping → slot selectors
-//   A1  run-start masks → each wave's last run start                   (team exchange 1)
-//   A2  chunk-start masks (255-cap of the carried run) → pair counts   (team exchange 2)
-//       → decoupled look-back on the blob size → header
-//   B   per wave and round, pairs are emitted branch-free: every slot writes (clz count,
-//       value) at its chunk's pair index (bcnt of the end mask) in ascending slot order, so a
-//       chunk's END slot writes last; one repair write per stream and lane rewrites the pair
-//       whose chunk began before the group (and any same-instruction collision).  The window
-//       is per wave, congruent (mod 16) with its destination, flushed with 16-byte stores.
-//       No workgroup barrier in pass B.
+//   A1  run-start masks → each wave's last run start; a per-round block test that rules the
+//       255-cap out for the message                                   (team exchange 1)
+//   A2  only if the cap may occur: chunk-start masks (255-cap of the carried run)
+//       → pair counts                                                  (team exchange 2)
+//       → output slot (or decoupled look-back on the blob size) → header
+//   B   per wave and round, every chunk start writes an entry (value, position) at its rank
+//       (a running per-lane address: one mul24 select between the entry and a lane-private
+//       junk dword); the flush forms pair k from entries k and k+1 (count = position
+//       difference) with 2-byte stores coalesced across the wave; the round's last chunk stays
+//       pending into the next round.  No workgroup barrier in pass B.
 // tools/emulate_encode.py restates this algorithm lane for lane (tests/test_emulator.py).
 #pragma once
 #include "tdt_device.h"
