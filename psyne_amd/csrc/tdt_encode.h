@@ -966,7 +966,11 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
         // per wave: 64 junk dwords (one per lane), then stream 0's pending entry + entries,
         // then stream 1's (EncLayout::WSTAGE)
         const uint32_t ebase = wst + 256u;
+#ifdef PSY_LANE_JUNK
         const uint32_t jl = wst + 4u * (uint32_t)lane;
+#else
+        const uint32_t jl = wst;  // one junk dword for the wave: same-address writes do not conflict
+#endif
         const uint32_t eoff1 = 4u * (1u + 64u * L0);  // stream 1's entry region (bytes)
         const uint32_t pb0 = (uint32_t)lane * Ls[0] + 256u, pb1 = (uint32_t)lane * Ls[1] + 256u - L0;
         auto emit5 = [&](uint32_t r, const uint4 &Tw, uint32_t C) __attribute__((always_inline)) {
@@ -1061,6 +1065,33 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
                 }
 #else
                 const bool even = ((uintptr_t)D & 1) == 0;
+#ifndef PSY_FLUSH1
+                // two pairs per lane and trip (k, k + 64): entries are read unconditionally at
+                // min(k, K) (entry f0 + K + 1 lies inside the stage), only the stores are masked
+                for (uint32_t k0 = 0; k0 < K; k0 += 128) {
+                    const uint32_t ka = k0 + (uint32_t)lane, kb = ka + 64u;
+                    const uint32_t ia = f0 + (ka < K ? ka : K), ib = f0 + (kb < K ? kb : K);
+                    const uint32_t a0 = *reinterpret_cast<const uint32_t *>(smem + eb + 4u * ia);
+                    const uint32_t a1 = *reinterpret_cast<const uint32_t *>(smem + eb + 4u * ia + 4u);
+                    const uint32_t b0 = *reinterpret_cast<const uint32_t *>(smem + eb + 4u * ib);
+                    const uint32_t b1 = *reinterpret_cast<const uint32_t *>(smem + eb + 4u * ib + 4u);
+                    const uint32_t pa = perm(a0, a1 - a0, 0x0c0c0700u);  // count, value
+                    const uint32_t pb = perm(b0, b1 - b0, 0x0c0c0700u);
+                    if (even) {
+                        if (ka < K) *reinterpret_cast<uint16_t *>(D + 2u * ka) = (uint16_t)pa;
+                        if (kb < K) *reinterpret_cast<uint16_t *>(D + 2u * kb) = (uint16_t)pb;
+                    } else {
+                        if (ka < K) {
+                            D[2u * ka] = (uint8_t)pa;
+                            D[2u * ka + 1u] = (uint8_t)(pa >> 8);
+                        }
+                        if (kb < K) {
+                            D[2u * kb] = (uint8_t)pb;
+                            D[2u * kb + 1u] = (uint8_t)(pb >> 8);
+                        }
+                    }
+                }
+#else
                 for (uint32_t k0 = 0; k0 < K; k0 += 64) {
                     const uint32_t k = k0 + (uint32_t)lane;
                     if (k < K) {
@@ -1075,6 +1106,7 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
                         }
                     }
                 }
+#endif
                 pi5[c] += K;
                 if (nent) {
                     const uint32_t el = __builtin_amdgcn_readfirstlane(*reinterpret_cast<const uint32_t *>(smem + eb + 4u * S[c]));
