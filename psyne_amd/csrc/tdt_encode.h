@@ -1065,7 +1065,8 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
                 }
 #else
                 const bool even = ((uintptr_t)D & 1) == 0;
-#ifndef PSY_FLUSH1
+#ifdef PSY_FLUSH2
+                // (diagnostic variant: measured neutral — more VALU and LDS reads for half the trips)
                 // two pairs per lane and trip (k, k + 64): entries are read unconditionally at
                 // min(k, K) (entry f0 + K + 1 lies inside the stage), only the stores are masked
                 for (uint32_t k0 = 0; k0 < K; k0 += 128) {
