@@ -1093,15 +1093,26 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
                     }
                 }
 #else
-                for (uint32_t k0 = 0; k0 < K; k0 += 64) {
+                // pair k = (count, value) from entries k and k+1; full 64-pair trips run without
+                // exec masking, the tail trip masked; the alignment test is hoisted out of the loop
+                auto pair_at = [&](uint32_t k) __attribute__((always_inline)) -> uint32_t {
+                    const uint32_t e0 = *reinterpret_cast<const uint32_t *>(smem + eb + 4u * (f0 + k));
+                    const uint32_t e1 = *reinterpret_cast<const uint32_t *>(smem + eb + 4u * (f0 + k + 1u));
+                    return perm(e0, e1 - e0, 0x0c0c0700u);  // count, value
+                };
+                if (even) {
+                    uint32_t k0 = 0;
+                    for (; k0 + 64u <= K; k0 += 64u) {
+                        const uint32_t k = k0 + (uint32_t)lane;
+                        *reinterpret_cast<uint16_t *>(D + 2u * k) = (uint16_t)pair_at(k);
+                    }
                     const uint32_t k = k0 + (uint32_t)lane;
-                    if (k < K) {
-                        const uint32_t e0 = *reinterpret_cast<const uint32_t *>(smem + eb + 4u * (f0 + k));
-                        const uint32_t e1 = *reinterpret_cast<const uint32_t *>(smem + eb + 4u * (f0 + k + 1u));
-                        const uint32_t pair = perm(e0, e1 - e0, 0x0c0c0700u);  // count, value
-                        if (even) {
-                            *reinterpret_cast<uint16_t *>(D + 2u * k) = (uint16_t)pair;
-                        } else {
+                    if (k < K) *reinterpret_cast<uint16_t *>(D + 2u * k) = (uint16_t)pair_at(k);
+                } else {
+                    for (uint32_t k0 = 0; k0 < K; k0 += 64) {
+                        const uint32_t k = k0 + (uint32_t)lane;
+                        if (k < K) {
+                            const uint32_t pair = pair_at(k);
                             D[2u * k] = (uint8_t)pair;
                             D[2u * k + 1u] = (uint8_t)(pair >> 8);
                         }
