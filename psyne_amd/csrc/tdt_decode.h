@@ -276,6 +276,7 @@ __device__ __forceinline__ void decode_fast(uint32_t *misc, uint8_t *smem, const
         }
     };
 
+    const bool dal16 = ((uintptr_t)dst & 15) == 0;
     uint32_t win = 0;
     for (uint32_t gwin = 0; gwin < ngroups; gwin += 64u * WR, ++win) {
         const uint32_t gen = win & 7u;
@@ -363,7 +364,10 @@ __device__ __forceinline__ void decode_fast(uint32_t *misc, uint8_t *smem, const
                                        perm(S[1], S[0], OA[2]) | perm(S[3], S[2], OB[2]),
                                        perm(S[1], S[0], OA[3]) | perm(S[3], S[2], OB[3]));
             const uint32_t g = g0 + lane;
-            if (g < ngroups) {
+            if (dal16 && 16ull * (g0 + 64u) <= wbytes) {
+                // a whole aligned round (uniform): one 16-byte store per lane, no per-lane tests
+                *reinterpret_cast<uint4 *>(dst + 16ull * g) = o;
+            } else if (g < ngroups) {
                 const uint64_t vb64 = wbytes - 16ull * g;
                 st16_any(dst + 16ull * g, o, vb64 >= 16 ? 16 : (int)vb64);
             }

@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 for v in "$@"; do
   lib=psyne_amd/libpsyne_tdt.so
   [ "$v" = base ] || lib=psyne_amd/libpsyne_tdt_x_$v.so
-  PSYNE_TDT_LIB=$lib timeout -s KILL 240 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS \
+  PSYNE_TDT_LIB=$lib timeout -s KILL 240 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_INSTS_SALU SQ_INSTS_VALU SQ_INSTS_LDS \
     SQ_LDS_BANK_CONFLICT SQ_WAIT_ANY SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE --output-format csv -d "$OUT/$v" -o "$v" -- \
     python3 bench.py --steps 1 --warmup 1 --cpu-seconds 0 > "$OUT/$v.log" 2>&1
   rc=$?; echo "pass $v rc=$rc"; [ $rc -eq 0 ] || exit $rc
