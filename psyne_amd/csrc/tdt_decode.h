@@ -45,7 +45,10 @@ struct DecodeArgs {
 };
 
 constexpr int kMaxRef = 16;  // referenced streams <= word_size <= 16
-constexpr int kDecWR = 2;    // rounds per window
+#ifndef PSY_DEC_WR
+#define PSY_DEC_WR 2
+#endif
+constexpr int kDecWR = PSY_DEC_WR;  // rounds per window
 constexpr int kHdrCache = 256;
 
 struct DecLayout {
