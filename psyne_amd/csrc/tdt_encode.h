@@ -1002,11 +1002,21 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
                 if (j > 0 && j % WPG == 0 && (uint32_t)j == L0) D = D1;  // stream 1 begins (uniform)
                 const bool s0 = (uint32_t)j < L0;
                 const uint32_t bit = (C >> j) & 1u;
-                const uint32_t ad = (uint32_t)__umul24(bit, D) + jl;
                 const uint32_t pos = (s0 ? pb0 : pb1) + (uint32_t)j;
+#ifndef PSY_SWEEP_C
+                // (inline asm keeps the running address: the compiler would rebuild it from a
+                // running count, one more VALU per slot)
+                uint32_t ad;
+                asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(ad) : "v"(bit), "v"(D), "v"(jl));
+                *reinterpret_cast<uint32_t *>(smem + ad) =
+                    perm(T[q], pos, ((uint32_t)(4 + t) << 24) | 0x000c0100u);
+                asm("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(D) : "v"(bit), "v"(D));
+#else
+                const uint32_t ad = (uint32_t)__umul24(bit, D) + jl;
                 *reinterpret_cast<uint32_t *>(smem + ad) =
                     perm(T[q], pos, ((uint32_t)(4 + t) << 24) | 0x000c0100u);
                 D += bit << 2;
+#endif
             }
             team_sync<1>();
             const bool last = gr <= ngroups - 1 && ngroups - 1 < gr + 64;  // the stream's end is here
