@@ -1112,6 +1112,14 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
                 };
                 if (even) {
                     uint32_t k0 = 0;
+#ifndef PSY_FLUSH_U1
+                    for (; k0 + 128u <= K; k0 += 128u) {  // two independent trips per iteration
+                        const uint32_t k = k0 + (uint32_t)lane;
+                        const uint32_t pa = pair_at(k), pb = pair_at(k + 64u);
+                        *reinterpret_cast<uint16_t *>(D + 2u * k) = (uint16_t)pa;
+                        *reinterpret_cast<uint16_t *>(D + 2u * k + 128u) = (uint16_t)pb;
+                    }
+#endif
                     for (; k0 + 64u <= K; k0 += 64u) {
                         const uint32_t k = k0 + (uint32_t)lane;
                         *reinterpret_cast<uint16_t *>(D + 2u * k) = (uint16_t)pair_at(k);
