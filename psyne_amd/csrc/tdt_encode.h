@@ -1023,6 +1023,9 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
 #pragma unroll
             for (int c = 0; c < 2; ++c) {
                 if (c == 1 && !ns2) break;
+#ifdef PSY_X_NOFLUSH
+                if (r < 1000u) continue;  // diagnostic: sweep only
+#endif
                 const uint32_t f0 = hp[c] ? 0u : 1u;
                 const uint32_t nent = S[c] + (hp[c] ? 1u : 0u);
                 const uint32_t K = nent ? nent - 1u : 0u;
@@ -1155,9 +1158,127 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
             }
             team_sync<1>();  // the entries are rewritten by the next round
         };
+
+#ifndef PSY_EMIT_V4
+        // ---------------------------------------------------------------- emit v6
+        // Resident messages with word size <= 4: as v5, but entries are u16 (value << 8 |
+        // stream position mod 256 — with Ls a multiple of 4 every round starts at a multiple of
+        // 256 positions, and consecutive chunk starts are 1..255 apart, so count = (e1 - e0) mod
+        // 256) and TWO rounds share one flush: the per-round flush bookkeeping (pointers, the
+        // last-entry read, the pending entry, loop set-up) is paid once per pair of rounds.
+        constexpr bool E6 = RES && WS <= 4;
+        const uint32_t eb6 = wst + 16u;
+        const uint32_t eoff6 = 2u * (1u + 128u * L0);  // stream 1's u16 region (bytes)
+        uint32_t s6[2] = {0, 0};  // entries of the current batch, per stream
+        uint32_t pend6[2] = {0, 0};
+#pragma unroll
+        for (int c = 0; c < 2; ++c) pend6[c] = ((pend[c] >> 24) << 8) | ((pend[c] - 256u + gw0 * Ls[c]) & 0xffu);
+        auto sweep6 = [&](const uint4 &Tw, uint32_t C) __attribute__((always_inline)) {
+            PSY_ASM_ROUND(B);
+            const uint32_t T[4] = {Tw.x, Tw.y, Tw.z, Tw.w};
+            const uint32_t c0 = popc(C & lowL0);
+            const uint32_t pc = c0 | (popc(C >> L0) << 16);
+            const uint32_t pinc = wave_incl_scan<OpAdd>(pc);
+            const uint32_t pexc = pinc - pc;
+            const uint32_t Stot = rdlane(pinc, 63);
+            const uint32_t D0 = eb6 + 2u * (1u + s6[0] + (pexc & 0xffffu)) - jl;
+            const uint32_t D1 = eb6 + eoff6 + 2u * (1u + s6[1] + (pexc >> 16)) - jl;
+            uint32_t D = L0 == 0 ? D1 : D0;
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const int q = j & 3, t = j >> 2;
+                if (j > 0 && j % WPG == 0 && (uint32_t)j == L0) D = D1;  // stream 1 begins (uniform)
+                const bool s0 = (uint32_t)j < L0;
+                const uint32_t bit = (C >> j) & 1u;
+                const uint32_t pos = (s0 ? pb0 : pb1) + (uint32_t)j;
+                uint32_t ad;
+                asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(ad) : "v"(bit), "v"(D), "v"(jl));
+                *reinterpret_cast<uint16_t *>(smem + ad) = (uint16_t)perm(T[q], pos, 0x0c0c0000u | ((uint32_t)(4 + t) << 8));
+                asm("v_lshl_add_u32 %0, %1, 1, %2" : "=v"(D) : "v"(bit), "v"(D));
+            }
+            s6[0] += Stot & 0xffffu;
+            s6[1] += Stot >> 16;
+        };
+        // flush the batch; last: the stream ends in it
+        auto flush6 = [&](bool last) __attribute__((always_inline)) {
+            team_sync<1>();
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                if (c == 1 && !ns2) break;
+                const uint32_t f0 = hp[c] ? 0u : 1u;
+                const uint32_t nent = s6[c] + (hp[c] ? 1u : 0u);
+                const uint32_t K = nent ? nent - 1u : 0u;
+                const uint32_t eb = eb6 + (c ? eoff6 : 0u);
+                uint8_t *const Dp = dst + sdata[c] + 2ull * pi5[c];
+                auto pair_at = [&](uint32_t k) __attribute__((always_inline)) -> uint32_t {
+                    const uint32_t e0 = *reinterpret_cast<const uint16_t *>(smem + eb + 2u * (f0 + k));
+                    const uint32_t e1 = *reinterpret_cast<const uint16_t *>(smem + eb + 2u * (f0 + k + 1u));
+                    return perm(e0, e1 - e0, 0x0c0c0500u);  // count = (e1 - e0) mod 256, value
+                };
+                if (((uintptr_t)Dp & 1) == 0) {
+                    uint32_t k0 = 0;
+                    for (; k0 + 128u <= K; k0 += 128u) {
+                        const uint32_t k = k0 + (uint32_t)lane;
+                        const uint32_t pa = pair_at(k), pb = pair_at(k + 64u);
+                        *reinterpret_cast<uint16_t *>(Dp + 2u * k) = (uint16_t)pa;
+                        *reinterpret_cast<uint16_t *>(Dp + 2u * k + 128u) = (uint16_t)pb;
+                    }
+                    for (; k0 + 64u <= K; k0 += 64u) {
+                        const uint32_t k = k0 + (uint32_t)lane;
+                        *reinterpret_cast<uint16_t *>(Dp + 2u * k) = (uint16_t)pair_at(k);
+                    }
+                    const uint32_t k = k0 + (uint32_t)lane;
+                    if (k < K) *reinterpret_cast<uint16_t *>(Dp + 2u * k) = (uint16_t)pair_at(k);
+                } else {
+                    for (uint32_t k0 = 0; k0 < K; k0 += 64) {
+                        const uint32_t k = k0 + (uint32_t)lane;
+                        if (k < K) {
+                            const uint32_t pair = pair_at(k);
+                            Dp[2u * k] = (uint8_t)pair;
+                            Dp[2u * k + 1u] = (uint8_t)(pair >> 8);
+                        }
+                    }
+                }
+                pi5[c] += K;
+                if (nent) {
+                    const uint32_t el = __builtin_amdgcn_readfirstlane(*reinterpret_cast<const uint16_t *>(smem + eb + 2u * s6[c]));
+                    if (last) {  // the final chunk runs to the end of the stream
+                        if (lane == 0) {
+                            Dp[2u * K] = (uint8_t)(slen[c] - el);
+                            Dp[2u * K + 1u] = (uint8_t)(el >> 8);
+                        }
+                        pi5[c] += 1;
+                    }
+                    pend6[c] = el;
+                    hp[c] = true;
+                }
+                s6[c] = 0;
+            }
+            team_sync<1>();  // the entries are rewritten by the next batch
+        };
+#endif
 #endif
 
         if constexpr (RES) {
+#ifndef PSY_EMIT_V4
+          if constexpr (E6) {
+#pragma unroll
+            for (int r = 0; r < G; ++r) {
+                if ((uint32_t)r < RW) {
+                    if ((r & 1) == 0 && lane == 0) {  // batch start: the pending entries
+                        if (hp[0]) *reinterpret_cast<uint16_t *>(smem + eb6) = (uint16_t)pend6[0];
+                        if (ns2 && hp[1]) *reinterpret_cast<uint16_t *>(smem + eb6 + eoff6) = (uint16_t)pend6[1];
+                    }
+                    sweep6(dres[r], cres[r]);
+                    if ((r & 1) == 1 || (uint32_t)(r + 1) == RW) {
+                        const uint32_t gb = gw0 + (uint32_t)(r & ~1) * 64u, ge = gw0 + (uint32_t)r * 64u + 64u;
+                        flush6(gb <= ngroups - 1 && ngroups - 1 < ge);
+                    }
+                }
+            }
+          } else
+#endif
+          {
 #pragma unroll
             for (int r = 0; r < G; ++r) {
                 if ((uint32_t)r < RW) {
@@ -1170,6 +1291,7 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
 #endif
                 }
             }
+          }
         } else {
             // chunk masks are computed one round ahead (lane 63 needs the next round's)
             uint32_t rcarry[2] = {rin[0], rin[1]};
