@@ -48,6 +48,10 @@ struct tdt_ctx {
     // workspace: [0..64) counters (ticket, timeout), then one u64 look-back word per message
     uint8_t *ws = nullptr;
     size_t ws_bytes = 0;
+    // per-chunk sums of tdt_decode_slots' two-pass scan (one u64 per 8192 messages; stream-ordered
+    // like `ws`: one slotted decode per context at a time)
+    uint64_t *slot_sums = nullptr;
+    uint32_t slot_sums_n = 0;
     // host-path device buffers (tdt_analyze_host)
     uint8_t *h_dev = nullptr;
     size_t h_dev_bytes = 0;
@@ -483,6 +487,7 @@ void tdt_ctx_destroy(tdt_ctx *ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     if (ctx->ws) (void)hipFree(ctx->ws);
+    if (ctx->slot_sums) (void)hipFree(ctx->slot_sums);
     if (ctx->h_dev) (void)hipFree(ctx->h_dev);
     for (auto &h : ctx->hs) {
         if (h.stream) (void)hipStreamSynchronize(h.stream);
@@ -570,8 +575,12 @@ int tdt_encode_slots(tdt_ctx *ctx, const uint64_t *d_in_off, uint32_t n_msgs, ui
     if (!ctx) return set_err(TDT_E_ARG, "null context");
     if (!d_slot_off || (n_msgs && !d_in_off)) return set_err(TDT_E_ARG, "null offsets");
     HIPCHK(hipSetDevice(ctx->device));
-    hipLaunchKernelGGL((psy::tdt_slots_kernel<0>), dim3(1), dim3(1024), 0, (hipStream_t)stream, d_in_off, d_slot_off,
-                       n_msgs, (uint32_t)ctx->cfg.word_size);
+    if (n_msgs == 0) {  // d_in_off may be null for an empty batch
+        HIPCHK(hipMemsetAsync(d_slot_off, 0, 8, (hipStream_t)stream));
+        return TDT_OK;
+    }
+    hipLaunchKernelGGL(psy::tdt_encode_slots_kernel, dim3((n_msgs + 256) / 256), dim3(256), 0, (hipStream_t)stream,
+                       d_in_off, d_slot_off, n_msgs, (uint32_t)ctx->cfg.word_size);
     HIPCHK(hipGetLastError());
     return TDT_OK;
 }
@@ -586,8 +595,21 @@ int tdt_decode_slots(tdt_ctx *ctx, const uint8_t *d_in, const uint64_t *d_in_off
         if (st) return st;
     }
     HIPCHK(hipSetDevice(ctx->device));
-    hipLaunchKernelGGL((psy::tdt_slots_kernel<1>), dim3(1), dim3(1024), 0, (hipStream_t)stream, d_in_off, d_slot_off,
-                       n_msgs, 0u);
+    const uint32_t nb = (n_msgs + psy::kSlotChunk - 1) / psy::kSlotChunk;
+    if (nb > 1) {
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        if (nb > ctx->slot_sums_n) {
+            if (ctx->slot_sums) HIPCHK(hipFree(ctx->slot_sums));
+            ctx->slot_sums = nullptr;
+            HIPCHK(hipMalloc(&ctx->slot_sums, 8ull * nb));
+            ctx->slot_sums_n = nb;
+        }
+        hipLaunchKernelGGL(psy::tdt_slot_sums_kernel, dim3(nb - 1), dim3(psy::kSlotThreads), 0, (hipStream_t)stream,
+                           d_slot_off, ctx->slot_sums, n_msgs);
+        HIPCHK(hipGetLastError());
+    }
+    hipLaunchKernelGGL(psy::tdt_slot_scan_kernel, dim3(nb ? nb : 1), dim3(psy::kSlotThreads), 0, (hipStream_t)stream,
+                       d_slot_off, nb > 1 ? ctx->slot_sums : nullptr, n_msgs);
     HIPCHK(hipGetLastError());
     return TDT_OK;
 }

@@ -486,3 +486,39 @@ def test_decode_crafted_fast_path(orc):
         s, want = orc.decode(b)
         assert st[i] == s == 0, (i, st[i], s)
         assert got[i] == want, f"crafted blob {i}"
+
+
+@pytest.mark.parametrize("n", [0, 1, 8191, 8192, 8193, 20000, 50001])
+def test_slot_offsets_multi_chunk(n):
+    """tdt_encode_slots (closed form) and tdt_decode_slots (two-pass chunked scan, 8192
+    sizes per workgroup) against numpy cumsums, across chunk boundaries, with a non-zero
+    first input offset and with a slot array that is only 8-byte aligned (scalar path)."""
+    from psyne_amd._lib import check
+    rng = np.random.default_rng(n + 7)
+    codec = make_codec()
+    lib, h = codec._lib, codec._h
+    sizes = rng.integers(0, 40, n)
+    lead = 12
+    off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64) + lead
+    o = torch.from_numpy(off).cuda()
+    for shift in (0, 1):  # slot array 16-byte aligned / 8-byte aligned
+        raw = torch.full((n + 3,), -1, dtype=torch.int64, device="cuda")
+        sl = raw[shift:shift + n + 1]
+        check(lib.tdt_encode_slots(h, o.data_ptr(), n, sl.data_ptr(), 0))
+        torch.cuda.synchronize()
+        want = np.concatenate([[0], np.cumsum(2 * sizes + 28 + 16)]).astype(np.int64)
+        assert np.array_equal(sl.cpu().numpy(), want)
+    # decode side: UNCP blobs of the drawn payload sizes; decoded size = blob length - 4
+    blobs = [b"PCNU" + bytes(rng.integers(0, 256, int(s), dtype=np.uint8)) for s in sizes]
+    bb, bo = pack(blobs) if n else (np.zeros(1, np.uint8), np.zeros(1, np.int64))
+    dd, do = torch.from_numpy(bb).cuda(), torch.from_numpy(bo).cuda()
+    st = torch.zeros(max(n, 1), dtype=torch.int32, device="cuda")
+    for shift in (0, 1):
+        raw = torch.full((n + 3,), -1, dtype=torch.int64, device="cuda")
+        sl = raw[shift:shift + n + 1]
+        check(lib.tdt_decode_slots(h, dd.data_ptr(), do.data_ptr(), 0, n, sl.data_ptr(), st.data_ptr(), 0))
+        torch.cuda.synchronize()
+        want = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+        assert np.array_equal(sl.cpu().numpy(), want)
+        assert int(st[:n].abs().sum()) == 0
+        assert int(raw[shift + n + 1]) == -1  # nothing written past off[n]
