@@ -18,8 +18,8 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("PSYNE_ARCH", "gfx950")
 
 SOURCES = [CSRC / "tdt_api.hip"]
-DEPS = SOURCES + [CSRC / f for f in ("tdt_device.h", "tdt_encode.h", "tdt_decode.h", "tdt_log2.h",
-                                     "glibc_log2_data.h")] + [ROOT / "include" / "psyne_tdt.h"]
+# every header under csrc/ (tdt_api.hip includes them all, directly or not)
+DEPS = SOURCES + sorted(CSRC.glob("*.h")) + [ROOT / "include" / "psyne_tdt.h"]
 
 
 def needs_build() -> bool:

@@ -107,6 +107,10 @@ __device__ __forceinline__ uint32_t pk_max_u16(uint32_t a, uint32_t b) {
     return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(psy_u16x2, a),
                                                                   __builtin_bit_cast(psy_u16x2, b)));
 }
+// Two independent u16 adds per dword (v_pk_add_u16, no carry between the halves).
+__device__ __forceinline__ uint32_t pk_add_u16(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(psy_u16x2, a) + __builtin_bit_cast(psy_u16x2, b));
+}
 struct OpPkMax {
     __device__ __forceinline__ static uint32_t f(uint32_t a, uint32_t b) { return pk_max_u16(a, b); }
 };

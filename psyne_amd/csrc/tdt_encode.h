@@ -89,6 +89,20 @@ struct EncLayout {
     static constexpr int LOG_HC = HC == 1 ? 0 : HC == 2 ? 1 : HC == 4 ? 2 : HC == 8 ? 3 : 4;
     static constexpr int PS = 64 + 256 * HC;
     static constexpr int HIST = WS * PS * 4;
+    // Resident 512-thread teams with word size 2 or 4 use class histograms instead (H2):
+    // per byte position 128 rows (bin pair v>>1) x 16 lane classes (lane & 15) of u16x2 counters
+    // (bin v in half v & 1).  Bank = (16·row + class) mod 32, so the two lanes of a 32-lane group
+    // that share a class are the only ones that can meet on a bank: every ds_add_u32 is at worst
+    // 2-way, whatever the data (the dominant zero byte included).  A class counts at most
+    // 4 lanes x 8 waves x 8 rounds x 16/WS bytes per (position, bin) <= 2048, and the class sum
+    // at most wc <= 32768, so u16 halves never carry.
+#ifdef PSY_NO_H2
+    static constexpr bool H2 = false;
+#else
+    static constexpr bool H2 = TEAM == 512 && (WS == 2 || WS == 4);
+#endif
+    static constexpr int HIST2 = H2 ? WS * 8192 : 0;
+    static constexpr int HISTA = HIST > HIST2 ? HIST : HIST2;
     static constexpr int TB = (TEAM >= 256) ? (WS < 4 ? WS : 4) : 1;
     // one stream's pairs of one wave-round: alignment pad + 1024 pairs + one garbage pair
     static constexpr int WREGION = 16 + 2 * 64 * 16 + 16;
@@ -102,15 +116,15 @@ struct EncLayout {
     // Two phases share one region: histogram + entropy terms + log2 tables (dead once the
     // mapping is known) and pass B's per-wave staging windows.
     // + log2 tables (2 KiB) + the per-message term table for counts 1..64 (1 KiB)
-    static constexpr int ANALYSIS = HIST + TERMS + 2048 + 1024;
+    static constexpr int ANALYSIS = HISTA + TERMS + 2048 + 1024;
     static constexpr int REGION = STAGE > ANALYSIS ? STAGE : ANALYSIS;
     static constexpr int SLOTS = W * 8 * 4;
     static constexpr int MISC = 512;
-    static constexpr int WM = 128;  // mapping state (uint32)
+    static constexpr int WM = 176;  // mapping state (uint32)
     static constexpr int OFF_HIST = 0;
-    static constexpr int OFF_TERMS = HIST;
-    static constexpr int OFF_LOG2 = HIST + TERMS;
-    static constexpr int OFF_CTAB = HIST + TERMS + 2048;
+    static constexpr int OFF_TERMS = HISTA;
+    static constexpr int OFF_LOG2 = HISTA + TERMS;
+    static constexpr int OFF_CTAB = HISTA + TERMS + 2048;
     static constexpr int OFF_STAGE = 0;
     static constexpr int OFF_SLOTS = REGION;
     static constexpr int OFF_MISC = OFF_SLOTS + SLOTS;
@@ -122,9 +136,11 @@ struct EncLayout {
 // misc area (uint32 index)
 enum {
     M_MSG = 0, M_NS = 1, M_L0 = 2, M_K0 = 3, M_K1 = 4, M_SELA = 8 /*4*/, M_SELB = 12 /*4*/, M_EDA = 16,
-    M_EDB = 17, M_STATUS = 26, M_MAP = 32 /*16*/, M_ENT = 64 /*16 doubles*/, M_BASE = 96 /*u64*/,
-    M_SB = 100 /*16*/
+    M_EDB = 17, M_EXACT = 18, M_STATUS = 26, M_MAP = 32 /*16*/, M_ENT = 64 /*16 doubles*/, M_BASE = 96 /*u64*/,
+    M_SB = 100 /*16*/, M_PART = 128 /*24 doubles: per-wave entropy partials*/
 };
+// decision margin of the mapping fast path (>= 2000x the worst-case |fma chain - any-order sum|)
+constexpr double kTieMargin = 1e-9;
 // per-wave slots (uint32, 8 per wave): 0,1 max(last run start+1); 2,3 chunk-start count;
 // 4 chunk bits of the wave's first group (combined slot layout)
 
@@ -350,8 +366,13 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
         // v at position p adds 1 to copy (lane mod HC) of bin v — or, for v = 0 (dominant in
         // float tensors), to this lane's private zero bin — so one ds_add only sends two
         // lanes to the same address when they hold the same nonzero value.
+        constexpr bool H2 = RES && Lay::H2;
         uint32_t *hist = reinterpret_cast<uint32_t *>(smem + Lay::OFF_HIST);
-        for (int i = tid; i < WS * Lay::PS / 4; i += TEAM) reinterpret_cast<uint4 *>(hist)[i] = make_uint4(0, 0, 0, 0);
+        if constexpr (H2) {
+            for (int i = tid; i < Lay::HIST2 / 16; i += TEAM) reinterpret_cast<uint4 *>(hist)[i] = make_uint4(0, 0, 0, 0);
+        } else {
+            for (int i = tid; i < WS * Lay::PS / 4; i += TEAM) reinterpret_cast<uint4 *>(hist)[i] = make_uint4(0, 0, 0, 0);
+        }
         // glibc log2 tables → LDS (the bins' log2 evaluations read them with per-lane indices)
 #pragma unroll
         for (int k = 0; k < NL2; ++k)
@@ -359,18 +380,29 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
         team_sync<W>();
         const uint32_t zoff = (uint32_t)lane * 4u;
         const uint32_t coff = (64u + ((uint32_t)lane & (Lay::HC - 1))) * 4u;
+        const uint32_t cls4 = ((uint32_t)lane & 15u) * 4u;  // H2: this lane's class column
         auto hist_group = [&](const uint4 &d, uint32_t vb, bool full) __attribute__((always_inline)) {
             const uint32_t dw[4] = {d.x, d.y, d.z, d.w};
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
-                const uint32_t v = (dw[i >> 2] >> (8 * (i & 3))) & 0xffu;
-                const uint32_t ad = v ? (v << (Lay::LOG_HC + 2)) + coff : zoff;
+                const uint32_t x = dw[i >> 2];
+                const uint32_t s = 8u * (uint32_t)(i & 3);
+                uint32_t ad, inc;
+                if constexpr (H2) {
+                    ad = (((x >> (s + 1u)) & 0x7fu) << 6) | cls4;        // row v >> 1, class lane & 15
+                    inc = __umul24((x >> s) & 1u, 0xffffu) + 1u;          // half v & 1
+                } else {
+                    const uint32_t v = (x >> s) & 0xffu;
+                    ad = v ? (v << (Lay::LOG_HC + 2)) + coff : zoff;
+                    inc = 1u;
+                }
+                constexpr uint32_t PSTRIDE = H2 ? 8192u : (uint32_t)Lay::PS * 4u;
 #ifndef PSY_X_NOHIST
                 if (full || (uint32_t)i < vb)
 #else
                 if (vb == 12345u)
 #endif
-                    atomicAdd(reinterpret_cast<uint32_t *>(smem + Lay::OFF_HIST + (i % WS) * Lay::PS * 4 + ad), 1u);
+                    atomicAdd(reinterpret_cast<uint32_t *>(smem + Lay::OFF_HIST + (i % WS) * PSTRIDE + ad), inc);
             }
         };
         for_rounds([&](uint32_t r, uint4 &d, uint32_t &, auto) __attribute__((always_inline)) {
@@ -407,11 +439,90 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
             }
             ctab[2 * tid] = -prob;
         }
+        // H2: the class sums, read while ctab is being written (the rows are final).  Wave w
+        // sweeps rows [16·WS·w, 16·WS·(w+1)): per instruction 16 rows as one contiguous 1 KiB
+        // ds_read_b128 (conflict-free), a quad of lanes per row, then a quad reduction; lane j
+        // keeps the row of instruction j & 3: row 16·WS·w + 16·(j & 3) + (j >> 2), whose two bins
+        // (v even in the low half) it then turns into entropy terms.
+        uint32_t h2sum = 0;
+        if constexpr (H2) {
+            static_assert(W == 8, "H2 sweeps assume 8 waves");
+#pragma unroll
+            for (int k = 0; k < WS; ++k) {
+                const uint32_t R = (uint32_t)wv * 16u * WS + 16u * (uint32_t)k + ((uint32_t)lane >> 2);
+                const uint4 q = *reinterpret_cast<const uint4 *>(smem + Lay::OFF_HIST + R * 64u + ((uint32_t)lane & 3u) * 16u);
+                uint32_t s = pk_add_u16(pk_add_u16(q.x, q.y), pk_add_u16(q.z, q.w));
+                s = pk_add_u16(s, dpp_mov_self<0xb1>(s));  // quad_perm [1,0,3,2]
+                s = pk_add_u16(s, dpp_mov_self<0x4e>(s));  // quad_perm [2,3,0,1]
+                if (((uint32_t)lane & 3u) == (uint32_t)k) h2sum = s;
+            }
+        }
         team_sync<W>();
+        // (-prob, log2 prob) of a bin with count c
+        auto bin_terms = [&](uint32_t c, double &np, double &L) __attribute__((always_inline)) {
+            np = 0.0;
+            L = 0.0;
+            if (c > 64u) {
+                double prob;
+                {
+#pragma clang fp contract(off)
+                    prob = (double)c / total;
+                    L = psy_log2_glibc(prob, ltab, ltab + 128);
+                }
+                np = -prob;
+            } else if (c) {
+                const double2 t = reinterpret_cast<const double2 *>(ctab)[c - 1];
+                np = t.x;
+                L = t.y;
+            }
+        };
+        // Mapping decision fast path (DESIGN.md §4 "E").  When every position's terms fit one
+        // batch, each wave also sums its bins' rounded products np·L (any order) into a partial;
+        // the approximate entropies a_b differ from the reference's fma chains e_b by at most
+        // 2·256·2^-53·8 < 5e-13 (both are sums of <= 256 terms of a total <= 8 bits), and the
+        // means by as much, so when every |a_b - mean(a)| exceeds kTieMargin = 1e-9 the mapping
+        // a_b > mean(a) IS the reference's e_b > mean(e).  Otherwise (ties: constant or
+        // repeated-distribution data) wave 0 runs the exact chains on the stored terms.
+        constexpr bool ONEB = Lay::TB == WS && MODE != MODE_ANALYZE;
+        constexpr int NKB = (Lay::TB * 256 + TEAM - 1) / TEAM;  // bin batches per thread
+        double *part = reinterpret_cast<double *>(wm + M_PART);
+        auto wave_partial = [&](double x, int k) __attribute__((always_inline)) {
+#pragma unroll
+            for (int o = 32; o; o >>= 1) x += __shfl_xor(x, o);
+            if (lane == 0) part[H2 ? wv : k * W + wv] = x;
+        };
+#ifndef PSY_X_FIXMAP
         for (int q0 = 0; q0 < WS; q0 += Lay::TB) {
+#else
+        for (int q0 = 0; q0 < 0; q0 += Lay::TB) {  // diagnostic: no entropy terms / chains
+#endif
             if (q0 > 0) team_sync<W>();  // every wave's chain has read the previous batch
-            for (int i = tid; i < Lay::TB * 256; i += TEAM) {
-                const int b = q0 + i / 256;  // wave-uniform
+            if constexpr (H2) {
+                // TB == WS: one batch, every position
+                double acc = 0.0;
+                if (((uint32_t)lane & 3u) < (uint32_t)WS) {
+                    const uint32_t R = (uint32_t)wv * 16u * WS + 16u * ((uint32_t)lane & 3u) + ((uint32_t)lane >> 2);
+                    const uint32_t bi = R * 2u;  // bin index b·256 + v of the even bin
+                    double np0, L0, np1, L1;
+                    bin_terms(h2sum & 0xffffu, np0, L0);
+                    bin_terms(h2sum >> 16, np1, L1);
+                    if constexpr (MODE == MODE_ANALYZE) {
+                        if (a.hist_out) {
+                            a.hist_out[(uint64_t)msg * WS * 256 + bi] = h2sum & 0xffffu;
+                            a.hist_out[(uint64_t)msg * WS * 256 + bi + 1] = h2sum >> 16;
+                        }
+                    }
+                    reinterpret_cast<double2 *>(terms)[bi] = make_double2(np0, L0);
+                    reinterpret_cast<double2 *>(terms)[bi + 1] = make_double2(np1, L1);
+                    if constexpr (ONEB) acc = np0 * L0 + np1 * L1;
+                }
+                if constexpr (ONEB) wave_partial(acc, 0);
+            } else {
+#pragma unroll
+            for (int k = 0; k < NKB; ++k) {
+                const int i = tid + k * TEAM;
+                if (i >= Lay::TB * 256) break;  // wave-uniform
+                const int b = q0 + i / 256;     // wave-uniform
                 double np = 0.0, L = 0.0;
                 if (b < WS) {
                     uint32_t c = count(b, i & 255);
@@ -422,39 +533,66 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
                     if constexpr (MODE == MODE_ANALYZE) {
                         if (a.hist_out) a.hist_out[((uint64_t)msg * WS + b) * 256 + (i & 255)] = c;
                     }
-                    if (c > 64u) {
-                        double prob;
-                        {
-#pragma clang fp contract(off)
-                            prob = (double)c / total;
-                            L = psy_log2_glibc(prob, ltab, ltab + 128);
-                        }
-                        np = -prob;
-                    } else if (c) {
-                        const double2 t = reinterpret_cast<const double2 *>(ctab)[c - 1];
-                        np = t.x;
-                        L = t.y;
-                    }
+                    bin_terms(c, np, L);
                 }
                 terms[2 * i] = np;
                 terms[2 * i + 1] = L;
+                if constexpr (ONEB) wave_partial(np * L, k);
+            }
             }
             team_sync<W>();
-            if (wv == 0 && lane < Lay::TB && q0 + lane < WS) {
-                const int b = q0 + lane;
-                const double2 *tp = reinterpret_cast<const double2 *>(terms) + lane * 256;
-                double e = 0.0;
-#pragma unroll 16
-                for (int v = 0; v < 256; ++v) {
-                    const double2 t = tp[v];
-                    e = __builtin_fma(t.x, t.y, e);
+            if (wv == 0) {
+                bool exact = true;
+                if constexpr (ONEB) {
+                    // approximate entropies: partial j belongs to position (k·TEAM + 64·w) / 256
+                    double ap[WS];
+#pragma unroll
+                    for (int b = 0; b < WS; ++b) ap[b] = 0.0;
+                    if constexpr (H2) {
+#pragma unroll
+                        for (int w = 0; w < W; ++w) ap[(w * WS) / 8] += part[w];
+                    } else {
+#pragma unroll
+                        for (int k = 0; k < NKB; ++k)
+#pragma unroll
+                            for (int w = 0; w < W; ++w)
+                                if (k * TEAM + 64 * w < Lay::TB * 256) ap[(k * TEAM + 64 * w) / 256] += part[k * W + w];
+                    }
+                    double sa = 0.0;
+#pragma unroll
+                    for (int b = 0; b < WS; ++b) sa += ap[b];
+                    const double ma = sa / (double)WS;
+                    bool safe = true;
+#pragma unroll
+                    for (int b = 0; b < WS; ++b) safe = safe && __builtin_fabs(ap[b] - ma) > kTieMargin;
+                    if (safe) {
+                        exact = false;
+                        if (lane < WS) {
+                            double x = ap[0];
+#pragma unroll
+                            for (int b = 1; b < WS; ++b) x = lane == b ? ap[b] : x;
+                            wm[M_MAP + lane] = x > ma ? 1u : 0u;
+                        }
+                    }
                 }
-                reinterpret_cast<double *>(wm + M_ENT)[b] = e;
+                if (exact && lane < Lay::TB && q0 + lane < WS) {
+                    const int b = q0 + lane;
+                    const double2 *tp = reinterpret_cast<const double2 *>(terms) + lane * 256;
+                    double e = 0.0;
+#pragma unroll 16
+                    for (int v = 0; v < 256; ++v) {
+                        const double2 t = tp[v];
+                        e = __builtin_fma(t.x, t.y, e);
+                    }
+                    reinterpret_cast<double *>(wm + M_ENT)[b] = e;
+                }
+                if (exact) wm[M_EXACT] = 1u;  // uniform in wave 0
+                else if (lane == 0) wm[M_EXACT] = 0u;
             }
         }
         team_sync<1>();
-        // perform_clustering :507-525
-        if (tid == 0) {
+        // perform_clustering :507-525 (from the exact entropies, when the chains ran)
+        if (tid == 0 && wm[M_EXACT] != 0u) {
             const double *ent = reinterpret_cast<const double *>(wm + M_ENT);
             double sum = 0.0;
             for (int b = 0; b < WS; ++b) sum += ent[b];
@@ -465,6 +603,10 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
             }
             for (int b = 0; b < WS; ++b) wm[M_MAP + b] = ent[b] > thr ? 1u : 0u;
         }
+#ifdef PSY_X_FIXMAP
+        if (tid == 0)
+            for (int b = 0; b < WS; ++b) wm[M_MAP + b] = b < 3 ? 1u : 0u;  // diagnostic only
+#endif
         team_sync<1>();
         if constexpr (MODE == MODE_ANALYZE) {
             const uint64_t mb = (uint64_t)msg * WS;
@@ -1201,6 +1343,9 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
         };
         // flush the batch; last: the stream ends in it
         auto flush6 = [&](bool last) __attribute__((always_inline)) {
+#if defined(PSY_X_NOEMIT) || defined(PSY_X_NOFLUSH)
+            if (ngroups != 0xffffffffu) { s6[0] = s6[1] = 0; return; }  // diagnostic: no flush
+#endif
             team_sync<1>();
 #pragma unroll
             for (int c = 0; c < 2; ++c) {
@@ -1269,7 +1414,9 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
                         if (hp[0]) *reinterpret_cast<uint16_t *>(smem + eb6) = (uint16_t)pend6[0];
                         if (ns2 && hp[1]) *reinterpret_cast<uint16_t *>(smem + eb6 + eoff6) = (uint16_t)pend6[1];
                     }
+#ifndef PSY_X_NOEMIT
                     sweep6(dres[r], cres[r]);
+#endif
                     if ((r & 1) == 1 || (uint32_t)(r + 1) == RW) {
                         const uint32_t gb = gw0 + (uint32_t)(r & ~1) * 64u, ge = gw0 + (uint32_t)r * 64u + 64u;
                         flush6(gb <= ngroups - 1 && ngroups - 1 < ge);

@@ -522,3 +522,27 @@ def test_slot_offsets_multi_chunk(n):
         assert np.array_equal(sl.cpu().numpy(), want)
         assert int(st[:n].abs().sum()) == 0
         assert int(raw[shift + n + 1]) == -1  # nothing written past off[n]
+
+
+def test_mapping_ties_exact_fallback(orc):
+    """Messages whose byte-position entropies tie (or nearly tie) with their mean: the
+    kernel's any-order entropy sums cannot decide them (kTieMargin), so it must fall back to
+    the reference's sequential fma chains (tdt_compression.hpp:470-480) — compared here with
+    the oracle byte for byte, for the 512-lane (64 KiB) and the one-wave (1-4 KiB) teams."""
+    rng = np.random.default_rng(41)
+    msgs = []
+    for n in (1024, 4096, 65536):
+        w = n // 4
+        x = rng.integers(0, 256, w, dtype=np.uint8)
+        msgs.append(np.repeat(x, 4))                                  # 4 equal positions: exact tie
+        msgs.append(np.full(n, 0x3C, np.uint8))                       # constant: all entropies 0
+        y = rng.integers(0, 256, (w, 4), dtype=np.uint8)
+        y[:, 1] = y[:, 0]                                             # two equal positions
+        y[:, 3] = np.roll(y[:, 2], 1)                                 # same distribution, shifted
+        msgs.append(y.reshape(-1))
+        z = np.tile(np.arange(256, dtype=np.uint8), n // 256)         # every position uniform
+        msgs.append(z)
+        g = grad(rng, w)
+        msgs.append(g)
+    check_vs_oracle(orc, make_codec(), msgs)
+    check_vs_oracle(orc, make_codec(hint=1024), msgs)
