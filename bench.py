@@ -7,22 +7,40 @@ GRADIENTS generator of the reference's tdt_compression_benchmark.cpp:52-66), gen
 the device with a fixed seed.  One STEP = tdt_encode_slots + tdt_encode_batch_into over the
 whole batch (each blob in its own slot, lengths returned — one vector per message, as the
 reference's encode returns) followed by tdt_decode_slots + tdt_decode_batch_into of those
-blobs, inputs already resident in HBM.  Compression is on (bandwidth 10 Mbps < 100 Mbps threshold) and the
-mapping is computed from every word (the reference's sample_fraction = 1.0, deterministic).
+blobs, inputs already resident in HBM.  Compression is on (bandwidth 10 Mbps < 100 Mbps
+threshold) and the mapping is computed from every word (the reference's sample_fraction =
+1.0, deterministic).  --workload c2 / c4 run the other BASELINE configs (parity-test sizes
+for the headline; benched for the record, not as the metric).
 
 value = payload bytes round-tripped by all ranks / max-over-ranks wall time, in GiB/s.
 Multi-GPU: messages are independent, so each rank owns its own batch (weak scaling, no
-collective on the data path; the only collectives are the timing barriers/all-reduce).
+collective on the data path; the only collectives are the timing barriers and the gathers of
+the per-rank figures).
 
-Extra fields: roofline (dominant kernel, HIP events on the launch stream), cpu_baseline
-(the reference codec compiled where it lies, timed on this host), ratio and per-kernel ms.
+Measurement:
+  * kernels_ms: HIP events on the launch stream around EACH codec kernel alone (the slot
+    kernels are timed separately in slots_ms);
+  * roofline: the dominant kernel's algorithmic bytes per launch (Σ n + Σ E: input read once,
+    output written once) ÷ its own event time, against the 8 TB/s HBM peak; roofline.combined
+    is §8(d)'s 2(n+E) / (t_enc + t_dec);
+  * roofline.traffic: HBM bytes per launch from rocprofv3 FETCH/WRITE passes, taken only from a
+    profiles/*_traffic.json whose lib_sha256 matches the library being run (else null);
+  * cpu_baseline: the reference codec itself (oracle/_ref, compiled from the reference header
+    where it lies) on this host: 1 thread and all usable cores, sample_fraction 0.3 (the
+    reference default) and 1.0 (parity mode); value = the default-config all-cores row.  A
+    missing reference build is an error, not a silent fallback (--cpu-kind port times the C
+    restatement instead, labelled as such);
+  * host_inclusive (--host-inclusive): pinned host buffers through tdt_encode_host /
+    tdt_decode_host, every rank, next to the pinned hipMemcpyAsync H2D / D2H ceiling.
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import pathlib
+import subprocess
 import sys
 import time
 
@@ -39,8 +57,10 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--msgs", type=int, default=262144)
     ap.add_argument("--msg-bytes", type=int, default=65536)
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline duration (0 = skip)")
+    ap.add_argument("--cpu-seconds", type=float, default=3.0,
+                    help="target duration of EACH of the four CPU-baseline rows (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = all usable host cores")
+    ap.add_argument("--cpu-kind", choices=["reference", "port"], default="reference")
     ap.add_argument("--host-inclusive", action="store_true", help="also time pinned H2D+kernel+D2H")
     ap.add_argument("--seed", type=int, default=None)
     ap.add_argument("--workload", choices=["c2", "c3", "c4"], default="c3",
@@ -95,40 +115,72 @@ def zipf_sizes(n, seed, world=1, rank=0):
     return sizes[b[rank]:b[rank + 1]]
 
 
-def load_traffic(config_key):
-    """HBM bytes per launch measured with rocprofv3 PMC passes (profiles/*_traffic.json)."""
-    best = None
-    for p in sorted((ROOT / "profiles").glob("*_traffic.json")):
+def lib_sha256() -> str:
+    from psyne_amd import _lib
+    p = pathlib.Path(os.environ.get("PSYNE_TDT_LIB") or _lib.LIB_PATH)
+    return hashlib.sha256(p.read_bytes()).hexdigest()
+
+
+def load_traffic(config_key, sha):
+    """HBM bytes per launch measured with rocprofv3 PMC passes of THIS library build
+    (profiles/**/*traffic.json with a matching lib_sha256), or None."""
+    for p in sorted((ROOT / "profiles").glob("**/*traffic.json")):
         try:
             d = json.loads(p.read_text())
         except Exception:
             continue
-        if d.get("config") == config_key:
-            best = d
-    return best
+        if d.get("config") == config_key and d.get("lib_sha256") == sha:
+            d["_file"] = str(p.relative_to(ROOT))
+            return d
+    return None
 
 
-def cpu_baseline(data_u8, msg_bytes, target_s, threads):
-    """Time the REFERENCE codec (oracle/_ref, compiled from the reference header) on a
-    bounded sample of the same messages; fall back to the C restatement if absent."""
+def host_cores():
+    """(nproc, physical cores from lscpu) of this host."""
+    nproc = os.cpu_count() or 1
+    phys = None
+    try:
+        out = subprocess.run(["lscpu", "-p=CORE,SOCKET"], capture_output=True, text=True, timeout=20).stdout
+        cores = {tuple(l.split(",")) for l in out.splitlines() if l and not l.startswith("#")}
+        phys = len(cores) or None
+    except Exception:
+        pass
+    return nproc, phys
+
+
+def cpu_baseline(data_u8, msg_bytes, target_s, threads, kind):
+    """Four CPU rows of the REFERENCE codec (oracle/_ref, the reference header compiled where it
+    lies) on a bounded sample of the same messages: {1, `threads`} threads x sample_fraction
+    {0.3 (reference default), 1.0 (parity mode)}; one protocol object per thread."""
     import numpy as np
-    from oracle.oracle import Reference, Oracle
+    from oracle.oracle import Oracle, Reference
     n_sample = 512
     sample = data_u8[: n_sample * msg_bytes].cpu().numpy()
     off = np.arange(n_sample + 1, dtype=np.uint64) * msg_bytes
-    if Reference.available():
+    nproc, phys = host_cores()
+    rows = []
+    if kind == "reference":
+        if not Reference.available():
+            raise RuntimeError("cpu_baseline: oracle/_ref/libtdt_ref.so (the compiled reference) is missing; "
+                               "build it in the container that has /root/reference (make -C oracle) or pass "
+                               "--cpu-kind port")
         ref = Reference()
-        # calibrate on 1 thread, then scale reps to ~target_s on `threads` threads
-        t1, _ = ref.bench(sample[: 32 * msg_bytes], off[:33], sample_fraction=0.3, threads=1, reps=1)
-        per_msg = t1 / 32
-        reps = max(1, int(target_s * threads / (per_msg * n_sample)))
-        secs, enc = ref.bench(sample, off, sample_fraction=0.3, threads=threads, reps=reps)
-        payload = n_sample * msg_bytes * reps
-        return dict(value=payload / secs / 2**30, unit="GiB/s", cores=threads, kind="reference",
-                    sample="%d x %d B messages x %d reps, reference TDTCompressionProtocol (default "
-                           "TDTConfig, sample_fraction 0.3), encode+decode, one object per thread, %.1f s"
-                           % (n_sample, msg_bytes, reps, secs),
-                    ratio=float(payload / enc))
+        for sf in (0.3, 1.0):
+            t1, _ = ref.bench(sample[: 16 * msg_bytes], off[:17], sample_fraction=sf, threads=1, reps=1)
+            per_msg = t1 / 16
+            for thr in (1, threads):
+                reps = max(1, int(target_s * thr / (per_msg * n_sample)))
+                secs, enc = ref.bench(sample, off, sample_fraction=sf, threads=thr, reps=reps)
+                payload = n_sample * msg_bytes * reps
+                rows.append(dict(value=payload / secs / 2**30, unit="GiB/s", cores=thr, sample_fraction=sf,
+                                 seconds=round(secs, 2), msgs=n_sample * reps, ratio=float(payload / enc)))
+        main = next(r for r in rows if r["sample_fraction"] == 0.3 and r["cores"] == threads)
+        return dict(value=main["value"], unit="GiB/s", cores=threads, kind="reference",
+                    sample="%d x %d B messages (the benched payload's first %d), reference "
+                           "TDTCompressionProtocol encode+decode, default TDTConfig (sample_fraction 0.3), "
+                           "one object per thread, %d threads, %.1f s" % (n_sample, msg_bytes, n_sample, threads,
+                                                                         main["seconds"]),
+                    rows=rows, nproc=nproc, lscpu_physical_cores=phys)
     orc = Oracle()
     t0 = time.perf_counter()
     reps = 0
@@ -139,7 +191,88 @@ def cpu_baseline(data_u8, msg_bytes, target_s, threads):
         reps += 1
     secs = time.perf_counter() - t0
     return dict(value=n_sample * msg_bytes * reps / secs / 2**30, unit="GiB/s", cores=1, kind="port",
-                sample="%d x %d B messages x %d reps, oracle restatement, 1 thread" % (n_sample, msg_bytes, reps))
+                sample="%d x %d B messages x %d reps, oracle C restatement (sample_fraction 1.0), 1 thread"
+                       % (n_sample, msg_bytes, reps), nproc=nproc, lscpu_physical_cores=phys)
+
+
+def pcie_ceiling(torch, dev, nbytes=256 << 20, reps=5):
+    """Pinned hipMemcpyAsync ceilings (GB/s): H2D alone, D2H alone, and both directions at once
+    on two streams — the bound of the host-inclusive pipeline."""
+    h_src = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+    h_dst = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+    d_a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    d_b = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+
+    def timed(fn):
+        best = 1e9
+        for _ in range(reps):
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            fn()
+            torch.cuda.synchronize(dev)
+            best = min(best, time.perf_counter() - t0)
+        return best
+
+    with torch.cuda.stream(s1):
+        h2d = timed(lambda: d_a.copy_(h_src, non_blocking=True))
+        d2h = timed(lambda: h_dst.copy_(d_b, non_blocking=True))
+
+    def both():
+        with torch.cuda.stream(s1):
+            d_a.copy_(h_src, non_blocking=True)
+        with torch.cuda.stream(s2):
+            h_dst.copy_(d_b, non_blocking=True)
+    bi = timed(both)
+    return {"h2d_GBps": round(nbytes / h2d / 1e9, 2), "d2h_GBps": round(nbytes / d2h / 1e9, 2),
+            "bidir_GBps_each_way": round(nbytes / bi / 1e9, 2), "bytes": nbytes,
+            "note": "pinned host <-> device hipMemcpyAsync, best of %d" % reps}
+
+
+def host_inclusive(torch, codec, data, off, n, mb, reps=3):
+    """The TCP socket-buffer path: pinned host payloads -> tdt_encode_host (chunked, two
+    streams: H2D, kernel and D2H of neighbouring chunks overlap) -> pinned host blobs ->
+    tdt_decode_host -> pinned host payloads.  GiB/s of payload per direction, best of reps."""
+    from psyne_amd._lib import check
+    lib, h = codec._lib, codec._h
+    m = min(n, 32768)
+    src = torch.empty(m * mb, dtype=torch.uint8, pin_memory=True)
+    src.copy_(data[: m * mb])
+    hoff = torch.arange(m + 1, dtype=torch.int64) * mb
+    cap = m * codec.encode_bound(mb)
+    henc = torch.empty(cap, dtype=torch.uint8, pin_memory=True)
+    heoff = torch.empty(m + 1, dtype=torch.int64)
+    hst = torch.empty(m, dtype=torch.int32)
+    hdec = torch.empty(m * mb, dtype=torch.uint8, pin_memory=True)
+    hdoff = torch.empty(m + 1, dtype=torch.int64)
+    hdst = torch.empty(m, dtype=torch.int32)
+    torch.cuda.synchronize()
+    te, td = [], []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        check(lib.tdt_encode_host(h, src.data_ptr(), hoff.data_ptr(), m, henc.data_ptr(), cap, heoff.data_ptr(),
+                                  hst.data_ptr()))
+        te.append(time.perf_counter() - t0)
+        nb = int(heoff[-1])
+        t0 = time.perf_counter()
+        check(lib.tdt_decode_host(h, henc.data_ptr(), heoff.data_ptr(), m, hdec.data_ptr(), m * mb, hdoff.data_ptr(),
+                                  hdst.data_ptr()))
+        td.append(time.perf_counter() - t0)
+    ok = bool(torch.equal(hdec, src)) and int(hst.abs().sum()) == 0 and int(hdst.abs().sum()) == 0
+    b = m * mb
+    return {"msgs": m, "encode_GiBps": round(b / min(te) / 2**30, 3), "decode_GiBps": round(b / min(td) / 2**30, 3),
+            "roundtrip_GiBps": round(b / (min(te) + min(td)) / 2**30, 3), "encoded_bytes": nb, "ok": ok,
+            "note": "pinned host buffers; C-ABI tdt_encode_host/tdt_decode_host: 256 MiB chunks on two streams "
+                    "(H2D, kernel, D2H overlapped); payload bytes / wall"}
+
+
+def gather_obj(obj, world):
+    import torch.distributed as dist
+    if world == 1:
+        return [obj]
+    out = [None] * world
+    dist.all_gather_object(out, obj)
+    return out
 
 
 def main():
@@ -157,7 +290,6 @@ def main():
     torch.cuda.set_device(dev)
 
     from psyne_amd import TDTConfig, TdtCodec
-
     from psyne_amd.shard import all_true, reduce_max, reduce_sum
     n, mb = a.msgs, a.msg_bytes
     if a.workload == "c4":
@@ -200,29 +332,34 @@ def main():
     P = lambda t: t.data_ptr()
 
     def step(ev=None):
+        # events (on the launch stream): [0] slots [1] encode kernel [2] slots [3] decode kernel [4]
         if ev:
             ev[0].record(stream)
         check(lib.tdt_encode_slots(h, P(off), n, P(eslot), sp))
-        check(lib.tdt_encode_batch_into(h, P(data), P(off), n, P(enc), P(eslot), P(elen), P(est), sp))
         if ev:
             ev[1].record(stream)
-        check(lib.tdt_decode_slots(h, P(enc), P(eslot), P(elen), n, P(dslot), P(dst), sp))
-        check(lib.tdt_decode_batch_into(h, P(enc), P(eslot), P(elen), n, P(dec), P(dslot), P(dlen), P(dst), sp))
+        check(lib.tdt_encode_batch_into(h, P(data), P(off), n, P(enc), P(eslot), P(elen), P(est), sp))
         if ev:
             ev[2].record(stream)
+        check(lib.tdt_decode_slots(h, P(enc), P(eslot), P(elen), n, P(dslot), P(dst), sp))
+        if ev:
+            ev[3].record(stream)
+        check(lib.tdt_decode_batch_into(h, P(enc), P(eslot), P(elen), n, P(dec), P(dslot), P(dlen), P(dst), sp))
+        if ev:
+            ev[4].record(stream)
 
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize(dev)
     # correctness of the measured configuration (size-independent property): round trip
     ok = bool(torch.equal(dec, data)) and int(est.abs().sum()) == 0 and int(dst.abs().sum()) == 0
-    ok = ok and bool(torch.equal(dslot, off))
+    ok = ok and bool(torch.equal(dslot, off - off[0]))
     enc_bytes = int(elen.sum().item())
 
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(a.steps)]
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(5)] for _ in range(a.steps)]
     t0 = time.perf_counter()
     for k in range(a.steps):
         step(evs[k])
@@ -230,32 +367,36 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    t_enc = sum(e[0].elapsed_time(e[1]) for e in evs) / a.steps  # ms, encode launch incl. memset
-    t_dec = sum(e[1].elapsed_time(e[2]) for e in evs) / a.steps
-    elapsed = reduce_max(elapsed, dev)  # whole-job time = the slowest rank
+    avg = lambda i, j: sum(e[i].elapsed_time(e[j]) for e in evs) / a.steps  # ms
+    t_enc, t_dec = avg(1, 2), avg(3, 4)
+    t_eslot, t_dslot = avg(0, 1), avg(2, 3)
+    my_rate = payload * a.steps / elapsed / 2**30
+    job_elapsed = reduce_max(elapsed, dev)  # whole-job time = the slowest rank
     ok = all_true(ok, dev)
     job_payload = int(reduce_sum(payload, dev))
-
-    ms_per_step = elapsed / a.steps * 1e3
-    value = job_payload * a.steps / elapsed / 2**30
+    ms_per_step = job_elapsed / a.steps * 1e3
+    value = job_payload * a.steps / job_elapsed / 2**30
 
     host = None
-    if a.host_inclusive and rank == 0 and a.workload != "c4":
+    if a.host_inclusive and a.workload != "c4":
         host = host_inclusive(torch, codec, data, off, n, mb)
+        host["pcie_ceiling"] = pcie_ceiling(torch, dev)
+    per_rank = gather_obj({"rank": rank, "GiBps": round(my_rate, 3), "kernels_ms": [round(t_enc, 4), round(t_dec, 4)],
+                           "host_inclusive": host}, world)
 
     if rank == 0:
         alg = payload + enc_bytes  # algorithmic bytes per launch (read input once, write output once)
         dom, t_dom = ("tdt_encode_kernel", t_enc) if t_enc >= t_dec else ("tdt_decode_kernel", t_dec)
         achieved = alg / (t_dom * 1e-3) / 1e9
+        combined = 2 * alg / ((t_enc + t_dec) * 1e-3) / 1e9
         key = "%s_%dx%d" % (a.workload, n, mb)
-        tr = load_traffic(key) if a.workload == "c3" else None
-        traffic = None
-        if tr and dom in tr.get("kernels", {}):
-            traffic = tr["kernels"][dom].get("hbm_bytes_per_launch")
+        sha = lib_sha256()
+        tr = load_traffic(key, sha)
+        traffic = tr["kernels"][dom].get("hbm_bytes_per_launch") if tr and dom in tr.get("kernels", {}) else None
         cpu = None
         if a.cpu_seconds > 0 and a.workload == "c3":
             thr = a.cpu_threads or min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "1024")))
-            cpu = cpu_baseline(data, mb, a.cpu_seconds, thr)
+            cpu = cpu_baseline(data, mb, a.cpu_seconds, thr, a.cpu_kind)
         if a.workload == "c3":
             metric = "TDT encode+decode GiB/s (device-resident), 64 KiB msgs, 1/2/4/8 MI355X"
             workload = "C3: %d x %d B float32 gradient-like messages per GPU, encode+decode" % (n, mb)
@@ -288,10 +429,17 @@ def main():
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic,
-                         "algorithmic_bytes_per_launch": alg},
+                         "traffic_source": tr["_file"] if traffic is not None else
+                         "no PMC record for this library build (lib sha256 %s)" % sha[:16],
+                         "algorithmic_bytes_per_launch": alg,
+                         "combined": {"achieved": round(combined, 2), "frac": round(combined / HBM_PEAK_GBS, 4),
+                                      "def": "2(n+E) / (t_enc + t_dec), SURVEY.md 8(d)"}},
             "kernels_ms": {"encode": round(t_enc, 4), "decode": round(t_dec, 4)},
+            "slots_ms": {"encode_slots": round(t_eslot, 4), "decode_slots": round(t_dslot, 4)},
+            "lib_sha256": sha[:16],
             "compression_ratio": round(payload / enc_bytes, 4),
             "roundtrip_ok": ok,
+            "per_rank": per_rank,
             "cpu_baseline": cpu,
         }
         if host:
@@ -299,44 +447,6 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
-
-
-def host_inclusive(torch, codec, data, off, n, mb, reps=3):
-    """The TCP socket-buffer path: pinned host payloads -> tdt_encode_host (chunked, two
-    streams: H2D, kernel and D2H of neighbouring chunks overlap) -> pinned host blobs ->
-    tdt_decode_host -> pinned host payloads.  GiB/s of payload per direction, best of reps."""
-    import ctypes as C
-    from psyne_amd._lib import check
-    lib, h = codec._lib, codec._h
-    m = min(n, 32768)
-    src = torch.empty(m * mb, dtype=torch.uint8, pin_memory=True)
-    src.copy_(data[: m * mb])
-    hoff = torch.arange(m + 1, dtype=torch.int64) * mb
-    cap = m * codec.encode_bound(mb)
-    henc = torch.empty(cap, dtype=torch.uint8, pin_memory=True)
-    heoff = torch.empty(m + 1, dtype=torch.int64)
-    hst = torch.empty(m, dtype=torch.int32)
-    hdec = torch.empty(m * mb, dtype=torch.uint8, pin_memory=True)
-    hdoff = torch.empty(m + 1, dtype=torch.int64)
-    hdst = torch.empty(m, dtype=torch.int32)
-    torch.cuda.synchronize()
-    te, td = [], []
-    for _ in range(reps):
-        t0 = time.perf_counter()
-        check(lib.tdt_encode_host(h, src.data_ptr(), hoff.data_ptr(), m, henc.data_ptr(), cap, heoff.data_ptr(),
-                                  hst.data_ptr()))
-        te.append(time.perf_counter() - t0)
-        nb = int(heoff[-1])
-        t0 = time.perf_counter()
-        check(lib.tdt_decode_host(h, henc.data_ptr(), heoff.data_ptr(), m, hdec.data_ptr(), m * mb, hdoff.data_ptr(),
-                                  hdst.data_ptr()))
-        td.append(time.perf_counter() - t0)
-    ok = bool(torch.equal(hdec, src)) and int(hst.abs().sum()) == 0 and int(hdst.abs().sum()) == 0
-    b = m * mb
-    return {"msgs": m, "encode_GiBps": round(b / min(te) / 2**30, 3), "decode_GiBps": round(b / min(td) / 2**30, 3),
-            "roundtrip_GiBps": round(b / (min(te) + min(td)) / 2**30, 3), "encoded_bytes": nb, "ok": ok,
-            "note": "pinned host buffers; C-ABI tdt_encode_host/tdt_decode_host: 256 MiB chunks on two streams "
-                    "(H2D, kernel, D2H overlapped); payload bytes / wall"}
 
 
 if __name__ == "__main__":

@@ -130,13 +130,21 @@ int launch_encode(tdt_ctx *c, psy::EncodeArgs a, hipStream_t s) {
 }
 
 // Zero the counters + look-back words of a batch; `wsp` = an explicit workspace (host
-// pipeline slots) or null for the context's own.
-int prep(tdt_ctx *c, uint32_t n_msgs, hipStream_t s, uint8_t *&wsp) {
+// pipeline slots) or null for the context's own.  Slotted batches (no look-back, message id =
+// block index) only need the counter block for the error flags, zeroed once per context.
+int prep(tdt_ctx *c, uint32_t n_msgs, hipStream_t s, uint8_t *&wsp, bool lookback = true) {
     HIPCHK(hipSetDevice(c->device));
     if (!wsp) {
-        int st = ensure_ws(c, n_msgs);
+        const bool fresh = c->ws == nullptr;
+        int st = ensure_ws(c, lookback ? n_msgs : 0);
         if (st) return st;
         wsp = c->ws;
+        if (!lookback) {
+            if (fresh) HIPCHK(hipMemsetAsync(wsp, 0, kCounterBytes, s));
+            return TDT_OK;
+        }
+    } else if (!lookback) {
+        return TDT_OK;  // pipeline slot workspaces are zeroed by their own batch calls
     }
     HIPCHK(hipMemsetAsync(wsp, 0, kCounterBytes + 8ull * n_msgs, s));
     return TDT_OK;
@@ -155,7 +163,7 @@ int encode_common(tdt_ctx *c, int mode, const uint8_t *d_in, const uint64_t *d_i
     hipStream_t s = (hipStream_t)stream;
     std::unique_lock<std::mutex> lk(c->mu, std::defer_lock);
     if (!wsp) lk.lock();  // pipeline slots own their workspace
-    int st = prep(c, n_msgs, s, wsp);
+    int st = prep(c, n_msgs, s, wsp, !slotted);
     if (st) return st;
     psy::EncodeArgs a{};
     a.in = d_in;
@@ -201,7 +209,7 @@ int decode_common(tdt_ctx *c, bool sizes_only, const uint8_t *d_in, const uint64
     hipStream_t s = (hipStream_t)stream;
     std::unique_lock<std::mutex> lk(c->mu, std::defer_lock);
     if (!wsp) lk.lock();
-    int st = prep(c, n_msgs, s, wsp);
+    int st = prep(c, n_msgs, s, wsp, !(slotted || sizes_only));
     if (st) return st;
     psy::DecodeArgs a{};
     a.in = d_in;

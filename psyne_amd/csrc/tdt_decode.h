@@ -389,9 +389,14 @@ __global__ __launch_bounds__(64) void tdt_decode_kernel(DecodeArgs a) {
     const int lane = lane_id();
     PSY_PROF_BEGIN();
 
+    // look-back needs ids in dispatch order (atomic ticket); slotted outputs do not
     uint32_t msg = 0;
-    if (lane == 0) msg = atomicAdd(a.ticket, 1u);
-    msg = __builtin_amdgcn_readfirstlane(msg);
+    if constexpr (LB) {
+        if (lane == 0) msg = atomicAdd(a.ticket, 1u);
+        msg = __builtin_amdgcn_readfirstlane(msg);
+    } else {
+        msg = blockIdx.x;
+    }
     if (msg >= a.n_msgs) return;
     const uint64_t boff = a.in_off[msg];
     const uint64_t len = a.in_len ? a.in_len[msg] : a.in_off[msg + 1] - boff;

@@ -111,6 +111,9 @@ __device__ __forceinline__ uint32_t pk_max_u16(uint32_t a, uint32_t b) {
 __device__ __forceinline__ uint32_t pk_add_u16(uint32_t a, uint32_t b) {
     return __builtin_bit_cast(uint32_t, __builtin_bit_cast(psy_u16x2, a) + __builtin_bit_cast(psy_u16x2, b));
 }
+__device__ __forceinline__ uint32_t pk_sub_u16(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(psy_u16x2, a) - __builtin_bit_cast(psy_u16x2, b));
+}
 struct OpPkMax {
     __device__ __forceinline__ static uint32_t f(uint32_t a, uint32_t b) { return pk_max_u16(a, b); }
 };
@@ -129,6 +132,28 @@ __device__ __forceinline__ uint32_t ffbh_u32(uint32_t x) {
     uint32_t r;
     asm("v_ffbh_u32 %0, %1" : "=v"(r) : "v"(x));
     return r;
+}
+
+// f64 helpers: DPP moves of both halves (lanes whose source is outside the row get 0)
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double x) {
+    const uint64_t u = __builtin_bit_cast(uint64_t, x);
+    const uint32_t lo = dpp_mov<CTRL>((uint32_t)u), hi = dpp_mov<CTRL>((uint32_t)(u >> 32));
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+// lane 16r + 15 receives the sum of row r's 16 values (other lanes: partial sums)
+__device__ __forceinline__ double row_sum_f64(double x) {
+    x += dpp_f64<0x111>(x);  // row_shr:1
+    x += dpp_f64<0x112>(x);  // row_shr:2
+    x += dpp_f64<0x114>(x);  // row_shr:4
+    x += dpp_f64<0x118>(x);  // row_shr:8
+    return x;
+}
+__device__ __forceinline__ double readlane_f64(double x, int l) {
+    const uint64_t u = __builtin_bit_cast(uint64_t, x);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l);
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
 }
 
 template <class Op>

@@ -89,20 +89,7 @@ struct EncLayout {
     static constexpr int LOG_HC = HC == 1 ? 0 : HC == 2 ? 1 : HC == 4 ? 2 : HC == 8 ? 3 : 4;
     static constexpr int PS = 64 + 256 * HC;
     static constexpr int HIST = WS * PS * 4;
-    // Resident 512-thread teams with word size 2 or 4 use class histograms instead (H2):
-    // per byte position 128 rows (bin pair v>>1) x 16 lane classes (lane & 15) of u16x2 counters
-    // (bin v in half v & 1).  Bank = (16·row + class) mod 32, so the two lanes of a 32-lane group
-    // that share a class are the only ones that can meet on a bank: every ds_add_u32 is at worst
-    // 2-way, whatever the data (the dominant zero byte included).  A class counts at most
-    // 4 lanes x 8 waves x 8 rounds x 16/WS bytes per (position, bin) <= 2048, and the class sum
-    // at most wc <= 32768, so u16 halves never carry.
-#ifdef PSY_NO_H2
-    static constexpr bool H2 = false;
-#else
-    static constexpr bool H2 = TEAM == 512 && (WS == 2 || WS == 4);
-#endif
-    static constexpr int HIST2 = H2 ? WS * 8192 : 0;
-    static constexpr int HISTA = HIST > HIST2 ? HIST : HIST2;
+    static constexpr int HISTA = HIST;
     static constexpr int TB = (TEAM >= 256) ? (WS < 4 ? WS : 4) : 1;
     // one stream's pairs of one wave-round: alignment pad + 1024 pairs + one garbage pair
     static constexpr int WREGION = 16 + 2 * 64 * 16 + 16;
@@ -120,7 +107,7 @@ struct EncLayout {
     static constexpr int REGION = STAGE > ANALYSIS ? STAGE : ANALYSIS;
     static constexpr int SLOTS = W * 8 * 4;
     static constexpr int MISC = 512;
-    static constexpr int WM = 176;  // mapping state (uint32)
+    static constexpr int WM = 160;  // mapping state (uint32)
     static constexpr int OFF_HIST = 0;
     static constexpr int OFF_TERMS = HISTA;
     static constexpr int OFF_LOG2 = HISTA + TERMS;
@@ -137,7 +124,7 @@ struct EncLayout {
 enum {
     M_MSG = 0, M_NS = 1, M_L0 = 2, M_K0 = 3, M_K1 = 4, M_SELA = 8 /*4*/, M_SELB = 12 /*4*/, M_EDA = 16,
     M_EDB = 17, M_EXACT = 18, M_STATUS = 26, M_MAP = 32 /*16*/, M_ENT = 64 /*16 doubles*/, M_BASE = 96 /*u64*/,
-    M_SB = 100 /*16*/, M_PART = 128 /*24 doubles: per-wave entropy partials*/
+    M_SB = 100 /*16*/, M_PART = 128 /*16 doubles: per-wave entropy partials*/
 };
 // decision margin of the mapping fast path (>= 2000x the worst-case |fma chain - any-order sum|)
 constexpr double kTieMargin = 1e-9;
@@ -366,13 +353,8 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
         // v at position p adds 1 to copy (lane mod HC) of bin v — or, for v = 0 (dominant in
         // float tensors), to this lane's private zero bin — so one ds_add only sends two
         // lanes to the same address when they hold the same nonzero value.
-        constexpr bool H2 = RES && Lay::H2;
         uint32_t *hist = reinterpret_cast<uint32_t *>(smem + Lay::OFF_HIST);
-        if constexpr (H2) {
-            for (int i = tid; i < Lay::HIST2 / 16; i += TEAM) reinterpret_cast<uint4 *>(hist)[i] = make_uint4(0, 0, 0, 0);
-        } else {
-            for (int i = tid; i < WS * Lay::PS / 4; i += TEAM) reinterpret_cast<uint4 *>(hist)[i] = make_uint4(0, 0, 0, 0);
-        }
+        for (int i = tid; i < WS * Lay::PS / 4; i += TEAM) reinterpret_cast<uint4 *>(hist)[i] = make_uint4(0, 0, 0, 0);
         // glibc log2 tables → LDS (the bins' log2 evaluations read them with per-lane indices)
 #pragma unroll
         for (int k = 0; k < NL2; ++k)
@@ -380,29 +362,18 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
         team_sync<W>();
         const uint32_t zoff = (uint32_t)lane * 4u;
         const uint32_t coff = (64u + ((uint32_t)lane & (Lay::HC - 1))) * 4u;
-        const uint32_t cls4 = ((uint32_t)lane & 15u) * 4u;  // H2: this lane's class column
         auto hist_group = [&](const uint4 &d, uint32_t vb, bool full) __attribute__((always_inline)) {
             const uint32_t dw[4] = {d.x, d.y, d.z, d.w};
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
-                const uint32_t x = dw[i >> 2];
-                const uint32_t s = 8u * (uint32_t)(i & 3);
-                uint32_t ad, inc;
-                if constexpr (H2) {
-                    ad = (((x >> (s + 1u)) & 0x7fu) << 6) | cls4;        // row v >> 1, class lane & 15
-                    inc = __umul24((x >> s) & 1u, 0xffffu) + 1u;          // half v & 1
-                } else {
-                    const uint32_t v = (x >> s) & 0xffu;
-                    ad = v ? (v << (Lay::LOG_HC + 2)) + coff : zoff;
-                    inc = 1u;
-                }
-                constexpr uint32_t PSTRIDE = H2 ? 8192u : (uint32_t)Lay::PS * 4u;
+                const uint32_t v = (dw[i >> 2] >> (8 * (i & 3))) & 0xffu;
+                const uint32_t ad = v ? (v << (Lay::LOG_HC + 2)) + coff : zoff;
 #ifndef PSY_X_NOHIST
                 if (full || (uint32_t)i < vb)
 #else
                 if (vb == 12345u)
 #endif
-                    atomicAdd(reinterpret_cast<uint32_t *>(smem + Lay::OFF_HIST + (i % WS) * PSTRIDE + ad), inc);
+                    atomicAdd(reinterpret_cast<uint32_t *>(smem + Lay::OFF_HIST + (i % WS) * Lay::PS * 4 + ad), 1u);
             }
         };
         for_rounds([&](uint32_t r, uint4 &d, uint32_t &, auto) __attribute__((always_inline)) {
@@ -439,24 +410,6 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
             }
             ctab[2 * tid] = -prob;
         }
-        // H2: the class sums, read while ctab is being written (the rows are final).  Wave w
-        // sweeps rows [16·WS·w, 16·WS·(w+1)): per instruction 16 rows as one contiguous 1 KiB
-        // ds_read_b128 (conflict-free), a quad of lanes per row, then a quad reduction; lane j
-        // keeps the row of instruction j & 3: row 16·WS·w + 16·(j & 3) + (j >> 2), whose two bins
-        // (v even in the low half) it then turns into entropy terms.
-        uint32_t h2sum = 0;
-        if constexpr (H2) {
-            static_assert(W == 8, "H2 sweeps assume 8 waves");
-#pragma unroll
-            for (int k = 0; k < WS; ++k) {
-                const uint32_t R = (uint32_t)wv * 16u * WS + 16u * (uint32_t)k + ((uint32_t)lane >> 2);
-                const uint4 q = *reinterpret_cast<const uint4 *>(smem + Lay::OFF_HIST + R * 64u + ((uint32_t)lane & 3u) * 16u);
-                uint32_t s = pk_add_u16(pk_add_u16(q.x, q.y), pk_add_u16(q.z, q.w));
-                s = pk_add_u16(s, dpp_mov_self<0xb1>(s));  // quad_perm [1,0,3,2]
-                s = pk_add_u16(s, dpp_mov_self<0x4e>(s));  // quad_perm [2,3,0,1]
-                if (((uint32_t)lane & 3u) == (uint32_t)k) h2sum = s;
-            }
-        }
         team_sync<W>();
         // (-prob, log2 prob) of a bin with count c
         auto bin_terms = [&](uint32_t c, double &np, double &L) __attribute__((always_inline)) {
@@ -477,19 +430,19 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
             }
         };
         // Mapping decision fast path (DESIGN.md §4 "E").  When every position's terms fit one
-        // batch, each wave also sums its bins' rounded products np·L (any order) into a partial;
-        // the approximate entropies a_b differ from the reference's fma chains e_b by at most
-        // 2·256·2^-53·8 < 5e-13 (both are sums of <= 256 terms of a total <= 8 bits), and the
-        // means by as much, so when every |a_b - mean(a)| exceeds kTieMargin = 1e-9 the mapping
-        // a_b > mean(a) IS the reference's e_b > mean(e).  Otherwise (ties: constant or
-        // repeated-distribution data) wave 0 runs the exact chains on the stored terms.
+        // batch, wave 0 sums the rounded products np·L of each position in any order (16 bins per
+        // lane, then a 16-lane reduction): these approximate entropies a_b differ from the
+        // reference's fma chains e_b by at most 2·256·2^-53·8 < 5e-13 (both are sums of <= 256
+        // terms of a total <= 8 bits), the means by as much, so when every |a_b - mean(a)|
+        // exceeds kTieMargin = 1e-9 the mapping a_b > mean(a) IS the reference's e_b > mean(e).
+        // Otherwise (ties: constant or repeated-distribution data) wave 0 runs the exact chains.
         constexpr bool ONEB = Lay::TB == WS && MODE != MODE_ANALYZE;
         constexpr int NKB = (Lay::TB * 256 + TEAM - 1) / TEAM;  // bin batches per thread
         double *part = reinterpret_cast<double *>(wm + M_PART);
         auto wave_partial = [&](double x, int k) __attribute__((always_inline)) {
-#pragma unroll
-            for (int o = 32; o; o >>= 1) x += __shfl_xor(x, o);
-            if (lane == 0) part[H2 ? wv : k * W + wv] = x;
+            x = row_sum_f64(x);  // lane 16r + 15: row r's sum
+            const double t = readlane_f64(x, 15) + readlane_f64(x, 31) + readlane_f64(x, 47) + readlane_f64(x, 63);
+            if (lane == 0) part[k * W + wv] = t;
         };
 #ifndef PSY_X_FIXMAP
         for (int q0 = 0; q0 < WS; q0 += Lay::TB) {
@@ -497,27 +450,7 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
         for (int q0 = 0; q0 < 0; q0 += Lay::TB) {  // diagnostic: no entropy terms / chains
 #endif
             if (q0 > 0) team_sync<W>();  // every wave's chain has read the previous batch
-            if constexpr (H2) {
-                // TB == WS: one batch, every position
-                double acc = 0.0;
-                if (((uint32_t)lane & 3u) < (uint32_t)WS) {
-                    const uint32_t R = (uint32_t)wv * 16u * WS + 16u * ((uint32_t)lane & 3u) + ((uint32_t)lane >> 2);
-                    const uint32_t bi = R * 2u;  // bin index b·256 + v of the even bin
-                    double np0, L0, np1, L1;
-                    bin_terms(h2sum & 0xffffu, np0, L0);
-                    bin_terms(h2sum >> 16, np1, L1);
-                    if constexpr (MODE == MODE_ANALYZE) {
-                        if (a.hist_out) {
-                            a.hist_out[(uint64_t)msg * WS * 256 + bi] = h2sum & 0xffffu;
-                            a.hist_out[(uint64_t)msg * WS * 256 + bi + 1] = h2sum >> 16;
-                        }
-                    }
-                    reinterpret_cast<double2 *>(terms)[bi] = make_double2(np0, L0);
-                    reinterpret_cast<double2 *>(terms)[bi + 1] = make_double2(np1, L1);
-                    if constexpr (ONEB) acc = np0 * L0 + np1 * L1;
-                }
-                if constexpr (ONEB) wave_partial(acc, 0);
-            } else {
+            {
 #pragma unroll
             for (int k = 0; k < NKB; ++k) {
                 const int i = tid + k * TEAM;
@@ -544,42 +477,30 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
             if (wv == 0) {
                 bool exact = true;
                 if constexpr (ONEB) {
-                    // approximate entropies: partial j belongs to position (k·TEAM + 64·w) / 256
-                    double ap[WS];
+                    // approximate entropy of position b in lane b: partial (k, w) belongs to
+                    // position (k·TEAM + 64·w) / 256
+                    double apl = 0.0;
 #pragma unroll
-                    for (int b = 0; b < WS; ++b) ap[b] = 0.0;
-                    if constexpr (H2) {
+                    for (int k = 0; k < NKB; ++k)
 #pragma unroll
-                        for (int w = 0; w < W; ++w) ap[(w * WS) / 8] += part[w];
-                    } else {
-#pragma unroll
-                        for (int k = 0; k < NKB; ++k)
-#pragma unroll
-                            for (int w = 0; w < W; ++w)
-                                if (k * TEAM + 64 * w < Lay::TB * 256) ap[(k * TEAM + 64 * w) / 256] += part[k * W + w];
-                    }
+                        for (int w = 0; w < W; ++w)
+                            if (k * TEAM + 64 * w < Lay::TB * 256 && (k * TEAM + 64 * w) / 256 == lane)
+                                apl += part[k * W + w];
                     double sa = 0.0;
 #pragma unroll
-                    for (int b = 0; b < WS; ++b) sa += ap[b];
+                    for (int b = 0; b < WS; ++b) sa += readlane_f64(apl, b);
                     const double ma = sa / (double)WS;
-                    bool safe = true;
-#pragma unroll
-                    for (int b = 0; b < WS; ++b) safe = safe && __builtin_fabs(ap[b] - ma) > kTieMargin;
-                    if (safe) {
+                    const bool unsafe = lane < WS && !(__builtin_fabs(apl - ma) > kTieMargin);
+                    if (!__any(unsafe)) {
                         exact = false;
-                        if (lane < WS) {
-                            double x = ap[0];
-#pragma unroll
-                            for (int b = 1; b < WS; ++b) x = lane == b ? ap[b] : x;
-                            wm[M_MAP + lane] = x > ma ? 1u : 0u;
-                        }
+                        if (lane < WS) wm[M_MAP + lane] = apl > ma ? 1u : 0u;
                     }
                 }
                 if (exact && lane < Lay::TB && q0 + lane < WS) {
                     const int b = q0 + lane;
                     const double2 *tp = reinterpret_cast<const double2 *>(terms) + lane * 256;
                     double e = 0.0;
-#pragma unroll 16
+#pragma unroll 8
                     for (int v = 0; v < 256; ++v) {
                         const double2 t = tp[v];
                         e = __builtin_fma(t.x, t.y, e);
@@ -948,142 +869,7 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
             }
         }
 
-#ifdef PSY_EMIT_V4
-        // Emit the pairs of round r: Tw its slot word, C its chunk-start mask, nxt63 the chunk
-        // bits of the group after lane 63's (combined layout).
-        auto emit = [&](uint32_t r, const uint4 &Tw, uint32_t C, uint32_t nxt63) __attribute__((always_inline)) {
-#ifdef PSY_X_NOEMIT
-            if (r < 100) return;
-#endif
-            PSY_ASM_ROUND(B);
-            const uint32_t T[4] = {Tw.x, Tw.y, Tw.z, Tw.w};
-            const uint32_t g = gw0 + r * 64 + lane;
-            // the message does not end inside (or before the end of) this round
-            const bool inner = 16ull * (gw0 + r * 64 + 64) < n;
-            const uint32_t V = inner ? 0xffffu : vmask(vbytes(g));
-            const uint32_t rb[2] = {(gw0 + r * 64) * Ls[0], (gw0 + r * 64) * Ls[1]};
-            // last chunk start + 1 before each group (packed, round-relative; 0 = earlier)
-            const uint32_t cinc = wave_incl_scan<OpPkMax>(last_starts(C));
-            const uint32_t cexc = wave_shr1(cinc, 0u);
-            // chunk END mask: slot j ends a chunk when the stream's next slot starts one
-            const uint32_t nb = wave_shl1(C, nxt63);
-            uint32_t e = (C >> 1) & 0x7fffu;
-            if (L0 > 0) e = (e & ~(1u << (L0 - 1))) | ((nb & 1u) << (L0 - 1));
-            if (ns2) e |= ((nb >> L0) & 1u) << 15;
-            if (!inner) {
-                if (g == ngroups - 1) {  // the message's last group closes every chunk
-                    const uint32_t lv0 = popc(V & lowL0), lv1 = popc(V >> L0);
-                    e = (C >> 1) & V;
-                    if (lv0) e |= 1u << (lv0 - 1);
-                    if (ns2 && lv1) e |= 1u << (L0 + lv1 - 1);
-                }
-                e &= V;
-            }
-            // pair indices: packed sum-scan of chunk starts
-            const uint32_t pc = popc(C & lowL0) | (popc(C >> L0) << 16);
-            const uint32_t pinc = wave_incl_scan<OpAdd>(pc);
-            const uint32_t pexc = pinc - pc;
-            const uint32_t ptr = rdlane(pinc, 63);
-            const uint32_t C_l0 = rdlane(C, 0), V_l0 = rdlane(V, 0);
-            uint32_t k0c[2], ends[2], rbs[2], base[2];
-            uint64_t gdst[2];
-#pragma unroll
-            for (int c = 0; c < 2; ++c) {
-                const uint32_t off = c ? L0 : 0u;
-                const uint32_t dang = (((V_l0 >> off) & 1u) && !((C_l0 >> off) & 1u)) ? 1u : 0u;
-                const uint32_t dout = inner ? (((nxt63 >> off) & 1u) ? 0u : 1u) : 0u;
-                const uint32_t tot = (ptr >> (16 * c)) & 0xffffu;
-                k0c[c] = pr[c] - dang;
-                ends[c] = (Ls[c] == 0) ? 0u : tot + dang - dout;
-                gdst[c] = (uint64_t)(uintptr_t)dst + sdata[c] + 2ull * k0c[c];
-                rbs[c] = wst + c * Lay::WREGION + 16u + (uint32_t)(gdst[c] & 15);
-                const uint32_t fi = pr[c] + ((pexc >> (16 * c)) & 0xffffu) - (((C >> off) & 1u) ? 0u : 1u);
-                base[c] = rbs[c] + 2u * (fi - k0c[c]);
-            }
-            // Lanes past the message end write into the wave's junk pair.  Every other slot
-            // that is not a chunk END writes where a later write of the same lane (its chunk's
-            // END slot, ascending order), the repair below, or nothing that is flushed (index
-            // >= ends: the slots after a lane's last END in the final group) overwrites it.
-            if (!inner && V == 0) base[0] = base[1] = wst + 2u * Lay::WREGION;
-            const uint32_t E2 = spread2(e);
-            const uint32_t base1p = base[1] - 2u * popc(e & lowL0);
-            // sweep 1: every slot, ascending; count = distance to the last chunk start <= j
-#pragma unroll
-            for (int j = 0; j < 16; j += 2) {
-                const int q = j & 3, t = j >> 2;
-                const uint32_t ca = ffbh_u32(C << (31 - j)), cb = ffbh_u32(C << (30 - j));
-                const uint32_t pair =
-                    (perm(cb, ca, 0x0c040c00u) + 0x00010001u) |
-                    perm(T[q + 1], T[q], 0x0cu | ((uint32_t)t << 8) | (0x0cu << 16) | ((uint32_t)(4 + t) << 24));
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const int jj = j + h;
-                    const uint32_t ad = ((uint32_t)jj < L0 ? base[0] : base1p) +
-                                        (jj ? popc(E2 & ((1u << (2 * jj)) - 1u)) : 0u);
-                    *reinterpret_cast<uint16_t *>(smem + ad) = (uint16_t)(h ? (pair >> 16) : pair);
-                }
-            }
-            // sweep 2: the first pair ending in this group, per stream (its chunk may have begun
-            // in an earlier group; this also repairs same-instruction collisions)
-#pragma unroll
-            for (int c = 0; c < 2; ++c) {
-                if (Ls[c] == 0) continue;
-                const uint32_t off = c ? L0 : 0u;
-                const uint32_t ec = c ? (e >> L0) : (e & lowL0);
-                if (ec) {
-                    const uint32_t jf = lobit(ec);
-                    uint32_t cnt;
-                    if ((C >> off) & 1u) {
-                        cnt = jf + 1u;
-                    } else {
-                        const uint32_t cer = (cexc >> (16 * c)) & 0xffffu;
-                        const uint32_t lcp = cer ? rb[c] + cer : ccarry[c];  // last chunk start + 1
-                        cnt = g * Ls[c] + jf + 2u - lcp;
-                    }
-                    const uint32_t val = c ? (perm(T[1], T[0], fsA) | perm(T[3], T[2], fsB)) : (T[0] & 0xffu);
-                    *reinterpret_cast<uint16_t *>(smem + base[c]) = (uint16_t)((cnt & 0xffu) | (val << 8));
-                }
-            }
-            team_sync<1>();  // this wave's staging writes are visible to its other lanes
-#pragma unroll
-            for (int c = 0; c < 2; ++c) {
-                if (Ls[c] == 0) continue;
-                const uint32_t len = 2u * ends[c];
-#ifdef PSY_GUARDS
-                if (len && sdata[c] + 2ull * k0c[c] + len > E) {  // never for a consistent round
-                    if (lane == 0) atomicOr(a.errflags, 4u);
-                    continue;
-                }
-#endif
-                if (len) {
-                    // The window is congruent (mod 16) with the destination: the unaligned head
-                    // and tail bytes go out in ONE byte-store instruction (lanes 0-15 head, lanes
-                    // 32-47 tail), the body as aligned 16-byte stores (at most 2 per lane).
-                    uint8_t *const gd = dst + sdata[c] + 2ull * k0c[c];
-                    const uint32_t ra = (uint32_t)(gdst[c] & 15);
-                    const uint32_t head0 = (16u - ra) & 15u;
-                    const uint32_t head = head0 < len ? head0 : len;
-                    const uint32_t body16 = (len - head) >> 4;
-                    const uint32_t tail = len - head - 16u * body16;
-                    const uint32_t ht = (uint32_t)lane < 16u ? (uint32_t)lane : head + 16u * body16 + ((uint32_t)lane - 32u);
-                    if ((uint32_t)lane < head || ((uint32_t)lane - 32u) < tail) gd[ht] = smem[rbs[c] + ht];
-#pragma unroll
-                    for (uint32_t it = 0; it < 2; ++it) {
-                        const uint32_t k = (uint32_t)lane + 64u * it;
-                        if (k < body16)
-                            *reinterpret_cast<uint4 *>(gd + head + 16u * k) =
-                                *reinterpret_cast<const uint4 *>(smem + rbs[c] + head + 16u * k);
-                    }
-                }
-                pr[c] += (ptr >> (16 * c)) & 0xffffu;
-                const uint32_t ci = (rdlane(cinc, 63) >> (16 * c)) & 0xffffu;
-                if (ci) ccarry[c] = umax(ccarry[c], rb[c] + ci);
-            }
-            team_sync<1>();  // the window is rewritten by the next round
-        };
-#endif
 
-#ifndef PSY_EMIT_V4
         // ---------------------------------------------------------------- emit v5
         // Chunk-START entries: every chunk start writes entry = value << 24 | (position within
         // the round + 256) at its rank among the round's starts (slot 0 of each stream holds
@@ -1108,11 +894,7 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
         // per wave: 64 junk dwords (one per lane), then stream 0's pending entry + entries,
         // then stream 1's (EncLayout::WSTAGE)
         const uint32_t ebase = wst + 256u;
-#ifdef PSY_LANE_JUNK
-        const uint32_t jl = wst + 4u * (uint32_t)lane;
-#else
         const uint32_t jl = wst;  // one junk dword for the wave: same-address writes do not conflict
-#endif
         const uint32_t eoff1 = 4u * (1u + 64u * L0);  // stream 1's entry region (bytes)
         const uint32_t pb0 = (uint32_t)lane * Ls[0] + 256u, pb1 = (uint32_t)lane * Ls[1] + 256u - L0;
         auto emit5 = [&](uint32_t r, const uint4 &Tw, uint32_t C) __attribute__((always_inline)) {
@@ -1145,7 +927,6 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
                 const bool s0 = (uint32_t)j < L0;
                 const uint32_t bit = (C >> j) & 1u;
                 const uint32_t pos = (s0 ? pb0 : pb1) + (uint32_t)j;
-#ifndef PSY_SWEEP_C
                 // (inline asm keeps the running address: the compiler would rebuild it from a
                 // running count, one more VALU per slot)
                 uint32_t ad;
@@ -1153,12 +934,6 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
                 *reinterpret_cast<uint32_t *>(smem + ad) =
                     perm(T[q], pos, ((uint32_t)(4 + t) << 24) | 0x000c0100u);
                 asm("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(D) : "v"(bit), "v"(D));
-#else
-                const uint32_t ad = (uint32_t)__umul24(bit, D) + jl;
-                *reinterpret_cast<uint32_t *>(smem + ad) =
-                    perm(T[q], pos, ((uint32_t)(4 + t) << 24) | 0x000c0100u);
-                D += bit << 2;
-#endif
             }
             team_sync<1>();
             const bool last = gr <= ngroups - 1 && ngroups - 1 < gr + 64;  // the stream's end is here
@@ -1173,81 +948,7 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
                 const uint32_t K = nent ? nent - 1u : 0u;
                 const uint32_t eb = ebase + (c ? eoff1 : 0u);
                 uint8_t *const D = dst + sdata[c] + 2ull * pi5[c];
-#ifdef PSY_FLUSH_WIN
-                // (diagnostic variant, measured slower: 15.9 vs 14.5 ms — the extra LDS round trip
-                // costs more than the 2-byte stores it saves)
-                // Pairs go to an LDS window congruent (mod 16) with D — pair k at byte
-                // wst + (D mod 16) + 2k, always below the entries still to be read — and leave
-                // in 16-byte stores (a 2-byte store per pair costs the vector memory path 8x
-                // the instructions).  The final chunk of the stream, when it ends here, is one
-                // more pair: count = stream length - its start.
-                if (nent) {
-                    const uint32_t el = __builtin_amdgcn_readfirstlane(*reinterpret_cast<const uint32_t *>(smem + eb + 4u * S[c]));
-                    const uint32_t Kw = K + (last ? 1u : 0u);
-                    const uint32_t ra = (uint32_t)((uintptr_t)D & 15);
-                    const uint32_t wb = wst + ra;
-                    const uint32_t fin = ((slen[c] - (gr * Ls[c] + (el & 0xffffu) - 256u)) & 0xffu) | ((el >> 24) << 8);
-                    for (uint32_t k0 = 0; k0 < Kw; k0 += 64) {
-                        const uint32_t k = k0 + (uint32_t)lane;
-                        if (k < Kw) {
-                            const uint32_t e0 = *reinterpret_cast<const uint32_t *>(smem + eb + 4u * (f0 + k));
-                            const uint32_t e1 = *reinterpret_cast<const uint32_t *>(smem + eb + 4u * (f0 + k + 1u));
-                            const uint32_t pair = k < K ? perm(e0, e1 - e0, 0x0c0c0700u) : fin;  // count, value
-                            *reinterpret_cast<uint16_t *>(smem + wb + 2u * k) = (uint16_t)pair;
-                        }
-                    }
-                    team_sync<1>();
-                    // head and tail bytes in ONE byte-store instruction (lanes 0-15 head, lanes
-                    // 32-47 tail), the body as aligned 16-byte stores (at most 2 per lane)
-                    const uint32_t len = 2u * Kw;
-                    const uint32_t head0 = (16u - ra) & 15u;
-                    const uint32_t head = head0 < len ? head0 : len;
-                    const uint32_t body16 = (len - head) >> 4;
-                    const uint32_t tail = len - head - 16u * body16;
-                    const uint32_t ht = (uint32_t)lane < 16u ? (uint32_t)lane : head + 16u * body16 + ((uint32_t)lane - 32u);
-                    if ((uint32_t)lane < head || ((uint32_t)lane - 32u) < tail) D[ht] = smem[wb + ht];
-#pragma unroll
-                    for (uint32_t it = 0; it < 2; ++it) {
-                        const uint32_t k = (uint32_t)lane + 64u * it;
-                        if (k < body16)
-                            *reinterpret_cast<uint4 *>(D + head + 16u * k) =
-                                *reinterpret_cast<const uint4 *>(smem + wb + head + 16u * k);
-                    }
-                    pi5[c] += Kw;
-                    pend[c] = el - 64u * Ls[c];  // rebased to the next round
-                    hp[c] = true;
-                    team_sync<1>();  // the window is rewritten by the next stream
-                }
-#else
                 const bool even = ((uintptr_t)D & 1) == 0;
-#ifdef PSY_FLUSH2
-                // (diagnostic variant: measured neutral — more VALU and LDS reads for half the trips)
-                // two pairs per lane and trip (k, k + 64): entries are read unconditionally at
-                // min(k, K) (entry f0 + K + 1 lies inside the stage), only the stores are masked
-                for (uint32_t k0 = 0; k0 < K; k0 += 128) {
-                    const uint32_t ka = k0 + (uint32_t)lane, kb = ka + 64u;
-                    const uint32_t ia = f0 + (ka < K ? ka : K), ib = f0 + (kb < K ? kb : K);
-                    const uint32_t a0 = *reinterpret_cast<const uint32_t *>(smem + eb + 4u * ia);
-                    const uint32_t a1 = *reinterpret_cast<const uint32_t *>(smem + eb + 4u * ia + 4u);
-                    const uint32_t b0 = *reinterpret_cast<const uint32_t *>(smem + eb + 4u * ib);
-                    const uint32_t b1 = *reinterpret_cast<const uint32_t *>(smem + eb + 4u * ib + 4u);
-                    const uint32_t pa = perm(a0, a1 - a0, 0x0c0c0700u);  // count, value
-                    const uint32_t pb = perm(b0, b1 - b0, 0x0c0c0700u);
-                    if (even) {
-                        if (ka < K) *reinterpret_cast<uint16_t *>(D + 2u * ka) = (uint16_t)pa;
-                        if (kb < K) *reinterpret_cast<uint16_t *>(D + 2u * kb) = (uint16_t)pb;
-                    } else {
-                        if (ka < K) {
-                            D[2u * ka] = (uint8_t)pa;
-                            D[2u * ka + 1u] = (uint8_t)(pa >> 8);
-                        }
-                        if (kb < K) {
-                            D[2u * kb] = (uint8_t)pb;
-                            D[2u * kb + 1u] = (uint8_t)(pb >> 8);
-                        }
-                    }
-                }
-#else
                 // pair k = (count, value) from entries k and k+1; full 64-pair trips run without
                 // exec masking, the tail trip masked; the alignment test is hoisted out of the loop
                 auto pair_at = [&](uint32_t k) __attribute__((always_inline)) -> uint32_t {
@@ -1257,14 +958,12 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
                 };
                 if (even) {
                     uint32_t k0 = 0;
-#ifndef PSY_FLUSH_U1
                     for (; k0 + 128u <= K; k0 += 128u) {  // two independent trips per iteration
                         const uint32_t k = k0 + (uint32_t)lane;
                         const uint32_t pa = pair_at(k), pb = pair_at(k + 64u);
                         *reinterpret_cast<uint16_t *>(D + 2u * k) = (uint16_t)pa;
                         *reinterpret_cast<uint16_t *>(D + 2u * k + 128u) = (uint16_t)pb;
                     }
-#endif
                     for (; k0 + 64u <= K; k0 += 64u) {
                         const uint32_t k = k0 + (uint32_t)lane;
                         *reinterpret_cast<uint16_t *>(D + 2u * k) = (uint16_t)pair_at(k);
@@ -1281,7 +980,6 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
                         }
                     }
                 }
-#endif
                 pi5[c] += K;
                 if (nent) {
                     const uint32_t el = __builtin_amdgcn_readfirstlane(*reinterpret_cast<const uint32_t *>(smem + eb + 4u * S[c]));
@@ -1296,12 +994,10 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
                     pend[c] = el - 64u * Ls[c];  // rebased to the next round
                     hp[c] = true;
                 }
-#endif
             }
             team_sync<1>();  // the entries are rewritten by the next round
         };
 
-#ifndef PSY_EMIT_V4
         // ---------------------------------------------------------------- emit v6
         // Resident messages with word size <= 4: as v5, but entries are u16 (value << 8 |
         // stream position mod 256 — with Ls a multiple of 4 every round starts at a multiple of
@@ -1330,11 +1026,10 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
             for (int j = 0; j < 16; ++j) {
                 const int q = j & 3, t = j >> 2;
                 if (j > 0 && j % WPG == 0 && (uint32_t)j == L0) D = D1;  // stream 1 begins (uniform)
-                const bool s0 = (uint32_t)j < L0;
                 const uint32_t bit = (C >> j) & 1u;
-                const uint32_t pos = (s0 ? pb0 : pb1) + (uint32_t)j;
                 uint32_t ad;
                 asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(ad) : "v"(bit), "v"(D), "v"(jl));
+                const uint32_t pos = ((uint32_t)j < L0 ? pb0 : pb1) + (uint32_t)j;
                 *reinterpret_cast<uint16_t *>(smem + ad) = (uint16_t)perm(T[q], pos, 0x0c0c0000u | ((uint32_t)(4 + t) << 8));
                 asm("v_lshl_add_u32 %0, %1, 1, %2" : "=v"(D) : "v"(bit), "v"(D));
             }
@@ -1401,11 +1096,8 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
             }
             team_sync<1>();  // the entries are rewritten by the next batch
         };
-#endif
-#endif
 
         if constexpr (RES) {
-#ifndef PSY_EMIT_V4
           if constexpr (E6) {
 #pragma unroll
             for (int r = 0; r < G; ++r) {
@@ -1424,18 +1116,11 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
                 }
             }
           } else
-#endif
           {
 #pragma unroll
             for (int r = 0; r < G; ++r) {
                 if ((uint32_t)r < RW) {
-#ifndef PSY_EMIT_V4
                     emit5((uint32_t)r, dres[r], cres[r]);
-#else
-                    uint32_t nx = nfb;
-                    if (r + 1 < G && (uint32_t)(r + 1) < RW) nx = rdlane(cres[r + 1 < G ? r + 1 : r], 0);
-                    emit((uint32_t)r, dres[r], cres[r], nx);
-#endif
                 }
             }
           }
@@ -1460,11 +1145,7 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
                 uint4 Tn = make_uint4(0, 0, 0, 0);
                 uint32_t Cn = 0;
                 if (r + 1 < RW) Cn = chunk_of(r + 1, load_group(gw0 + (r + 1) * 64 + lane), Tn);
-#ifndef PSY_EMIT_V4
                 emit5(r, Tc, Cc);
-#else
-                emit(r, Tc, Cc, r + 1 < RW ? rdlane(Cn, 0) : nfb);
-#endif
                 Tc = Tn;
                 Cc = Cn;
             }

@@ -1,7 +1,11 @@
 #!/usr/bin/env python3
 """HBM traffic per launch from rocprofv3 --pmc passes -> profiles/<tag>_traffic.json.
 
-usage: python tools/traffic_json.py <pmc dir> <out.json> <config key>
+usage: python tools/traffic_json.py <pmc dir> <out.json> <config key> [library .so]
+
+The record carries the sha256 of the HIP library the passes ran (default
+psyne_amd/libpsyne_tdt.so); bench.py reports `roofline.traffic` only from a record whose hash
+matches the library it is running, so a traffic figure can never describe other code.
 
 FETCH_SIZE / WRITE_SIZE are reported in KB.  MI355X_MICROARCH.md §HBM: on gfx950 FETCH_SIZE
 reports exactly half the bytes of a wide (16 B/lane) coalesced streaming read, so it is
@@ -11,7 +15,9 @@ the dispatches of the kernel.
 import collections
 import csv
 import glob
+import hashlib
 import json
+import pathlib
 import sys
 
 
@@ -37,7 +43,9 @@ def main():
         # the largest instantiation of a kernel name is the main pass (sizes-only passes are tiny)
         if short not in kernels or ent["hbm_bytes_per_launch"] > kernels[short]["hbm_bytes_per_launch"]:
             kernels[short] = ent
-    res = {"config": key, "kernels": kernels,
+    lib = pathlib.Path(sys.argv[4] if len(sys.argv) > 4 else
+                       pathlib.Path(__file__).resolve().parent.parent / "psyne_amd" / "libpsyne_tdt.so")
+    res = {"config": key, "kernels": kernels, "lib_sha256": hashlib.sha256(lib.read_bytes()).hexdigest(),
            "method": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950 correction) and WRITE_SIZE in separate passes"}
     with open(out, "w") as f:
         json.dump(res, f, indent=1)
