@@ -99,7 +99,7 @@ struct EncLayout {
     static constexpr int WSTAGE_V5 = 256 + 4 * (2 + 64 * 16);
     static constexpr int WSTAGE = ((WSTAGE_V4 > WSTAGE_V5 ? WSTAGE_V4 : WSTAGE_V5) + 15) / 16 * 16;
     static constexpr int STAGE = W * WSTAGE;
-    static constexpr int TERMS = TB * 256 * 16;
+    static constexpr int TERMS = TEAM >= 256 ? TB * 256 * 16 : 0;  // one-wave teams: in registers
     // Two phases share one region: histogram + entropy terms + log2 tables (dead once the
     // mapping is known) and pass B's per-wave staging windows.
     // + log2 tables (2 KiB) + the per-message term table for counts 1..64 (1 KiB)
@@ -444,12 +444,57 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
             const double t = readlane_f64(x, 15) + readlane_f64(x, 31) + readlane_f64(x, 47) + readlane_f64(x, 63);
             if (lane == 0) part[k * W + wv] = t;
         };
-#ifndef PSY_X_FIXMAP
-        for (int q0 = 0; q0 < WS; q0 += Lay::TB) {
-#else
-        for (int q0 = 0; q0 < 0; q0 += Lay::TB) {  // diagnostic: no entropy terms / chains
+        // Teams whose terms take several batches (the one-wave small-message team, word size
+        // 8/16) first run the same decision from a sweep that keeps no terms: per position,
+        // each thread sums its bins' products, one partial per (position, wave).  The batched
+        // exact path below then only runs when that sweep finds a near-tie.
+        constexpr bool SWEEP = !ONEB && MODE != MODE_ANALYZE && W * WS <= 16;
+        uint32_t nbatch = WS;  // positions the exact path covers (0: decided by the sweep)
+        if constexpr (SWEEP) {
+#pragma unroll 1
+            for (int b = 0; b < WS; ++b) {
+                double acc = 0.0;
+#pragma unroll
+                for (int k = 0; k < (256 + TEAM - 1) / TEAM; ++k) {
+                    const int v = tid + k * TEAM;
+                    if (v >= 256) break;  // wave-uniform
+                    uint32_t c = count(b, v);
+                    if (v < 64) {  // wave-uniform: bin 0 adds the 64 per-lane zero bins
+                        const uint32_t z = wave_reduce<OpAdd>(hist[b * Lay::PS + lane]);
+                        if (lane == 0) c += z;
+                    }
+                    double np, L;
+                    bin_terms(c, np, L);
+                    acc += np * L;
+                }
+                wave_partial(acc, b);  // part[b·W + wv]
+            }
+            team_sync<W>();
+            if (wv == 0) {
+                double apl = 0.0;
+#pragma unroll
+                for (int w = 0; w < W; ++w)
+                    if (lane < WS) apl += part[lane * W + w];
+                double sa = 0.0;
+#pragma unroll
+                for (int b = 0; b < WS; ++b) sa += readlane_f64(apl, b);
+                const double ma = sa / (double)WS;
+                const bool unsafe = lane < WS && !(__builtin_fabs(apl - ma) > kTieMargin);
+                const bool fast = !__any(unsafe);
+                if (fast && lane < WS) wm[M_MAP + lane] = apl > ma ? 1u : 0u;
+                if (lane == 0) wm[M_EXACT] = fast ? 0u : 1u;
+            }
+            team_sync<W>();
+            nbatch = wm[M_EXACT] ? (uint32_t)WS : 0u;  // uniform
+        }
+#ifdef PSY_X_FIXMAP
+        nbatch = 0;  // diagnostic: no entropy terms / chains
 #endif
+        for (int q0 = 0; (uint32_t)q0 < nbatch; q0 += Lay::TB) {
             if (q0 > 0) team_sync<W>();  // every wave's chain has read the previous batch
+            // one-wave teams keep their bins' terms in registers (no LDS terms array): bin v
+            // = 64·k + lane, read back in bin order by the chain through readlane
+            double rnp[W == 1 ? NKB : 1], rL[W == 1 ? NKB : 1];
             {
 #pragma unroll
             for (int k = 0; k < NKB; ++k) {
@@ -468,8 +513,13 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
                     }
                     bin_terms(c, np, L);
                 }
-                terms[2 * i] = np;
-                terms[2 * i + 1] = L;
+                if constexpr (W == 1) {
+                    rnp[k] = np;
+                    rL[k] = L;
+                } else {
+                    terms[2 * i] = np;
+                    terms[2 * i + 1] = L;
+                }
                 if constexpr (ONEB) wave_partial(np * L, k);
             }
             }
@@ -496,7 +546,18 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
                         if (lane < WS) wm[M_MAP + lane] = apl > ma ? 1u : 0u;
                     }
                 }
-                if (exact && lane < Lay::TB && q0 + lane < WS) {
+                if constexpr (W == 1) {
+                    static_assert(Lay::TB == 1, "one-wave teams run one position per batch");
+                    if (exact) {  // uniform: every lane runs the chain on readlane operands
+                        double e = 0.0;
+#pragma unroll
+                        for (int k = 0; k < NKB; ++k)
+#pragma unroll 8
+                            for (int l = 0; l < 64; ++l)
+                                e = __builtin_fma(readlane_f64(rnp[k], l), readlane_f64(rL[k], l), e);
+                        if (lane == 0) reinterpret_cast<double *>(wm + M_ENT)[q0] = e;
+                    }
+                } else if (exact && lane < Lay::TB && q0 + lane < WS) {
                     const int b = q0 + lane;
                     const double2 *tp = reinterpret_cast<const double2 *>(terms) + lane * 256;
                     double e = 0.0;
