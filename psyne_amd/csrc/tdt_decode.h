@@ -184,22 +184,32 @@ __global__ __launch_bounds__(256) void tdt_decode_sizes_kernel(DecodeArgs a) {
 // group's segments (dword reads) and v_perm's them into word order (recombine :614-637).
 constexpr int kFastWR = kDecWR;
 
-__device__ __forceinline__ void decode_fast(uint32_t *misc, uint8_t *smem, const uint8_t *blob, const uint8_t *blim,
-                                            uint8_t *dst, uint32_t ngroups, uint64_t wbytes, uint32_t WPG,
-                                            uint32_t nref, const uint32_t (&OA)[4], const uint32_t (&OB)[4]) {
+// Parameters of a fast-path blob (parse_fast): referenced streams r = 0, 1 (stream 1 absent
+// when !two) with seg[r] = WPG·k_r bytes per 16-byte group, np[r] pairs at blob offset soff[r].
+struct FastHdr {
+    uint32_t kind;  // 0: not fast (lane-0 parser + generic path), 1: UNCP, 2: TDT fast path
+    uint32_t orig, ws, two;
+    uint32_t seg[2], np[2], soff[2];
+    uint32_t OA[4], OB[4];
+    uint64_t osize;
+};
+
+__device__ __forceinline__ void decode_fast(const FastHdr &H, uint8_t *smem, const uint8_t *blob, const uint8_t *blim,
+                                            uint8_t *dst, uint32_t ngroups, uint64_t wbytes) {
     using Lay = DecLayout;
     constexpr uint32_t WR = kFastWR;
     const uint32_t lane = (uint32_t)lane_id();
     PSY_PROF_BEGIN();
     uint16_t *heads = reinterpret_cast<uint16_t *>(smem + Lay::OFF_HEADS);
     uint8_t *planes = smem + Lay::OFF_PLANES;
-    const bool two = nref == 2;
-    const uint32_t seg[2] = {WPG * (uint32_t)__builtin_amdgcn_readfirstlane(misc[D_K + 0]),
-                             two ? WPG * (uint32_t)__builtin_amdgcn_readfirstlane(misc[D_K + 1]) : 0u};
-    const uint32_t np[2] = {(uint32_t)__builtin_amdgcn_readfirstlane(misc[D_NP + 0]),
-                            two ? (uint32_t)__builtin_amdgcn_readfirstlane(misc[D_NP + 1]) : 0u};
-    const uint32_t soff[2] = {(uint32_t)__builtin_amdgcn_readfirstlane(misc[D_SOFF + 0]),
-                              two ? (uint32_t)__builtin_amdgcn_readfirstlane(misc[D_SOFF + 1]) : 0u};
+    // (every field is wave-uniform: readfirstlane keeps them in SGPRs)
+    auto U = [](uint32_t x) -> uint32_t { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); };
+    const bool two = U(H.two) != 0;
+    const uint32_t seg[2] = {U(H.seg[0]), two ? U(H.seg[1]) : 0u};
+    const uint32_t np[2] = {U(H.np[0]), two ? U(H.np[1]) : 0u};
+    const uint32_t soff[2] = {U(H.soff[0]), two ? U(H.soff[1]) : 0u};
+    const uint32_t OA[4] = {U(H.OA[0]), U(H.OA[1]), U(H.OA[2]), U(H.OA[3])};
+    const uint32_t OB[4] = {U(H.OB[0]), U(H.OB[1]), U(H.OB[2]), U(H.OB[3])};
     const uint32_t wlen[2] = {WR * 64u * seg[0], WR * 64u * seg[1]};
     const uint32_t hbase[2] = {(uint32_t)Lay::OFF_HEADS, (uint32_t)Lay::OFF_HEADS + 2u * (wlen[0] + 16u)};
     // fill lane
@@ -209,13 +219,14 @@ __device__ __forceinline__ void decode_fast(uint32_t *misc, uint8_t *smem, const
     const uint32_t f_lb = f1 ? 4u * seg[0] : 0u;  // first lane of this lane's stream plane
     const uint32_t fh = (f1 ? hbase[1] : hbase[0]) + 2u * fu;
     const uint32_t last_lane0 = 4u * seg[0] - 1u;  // lane holding stream 0's last plane byte
-    // recombine: S dword d = plane bytes sd_pb[d] + lane·sd_mul[d] (4 bytes of one stream)
+    // recombine: S dword d (S = the group's seg[0] stream-0 bytes, then its seg[1] stream-1
+    // bytes) = plane bytes sd_pb[d] + lane·sd_mul[d] (4 bytes of one stream: seg[r] % 4 == 0)
     uint32_t sd_pb[4], sd_mul[4];
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
-        const uint32_t e = __builtin_amdgcn_readfirstlane(misc[D_SB + 4 * d]);
-        const uint32_t r = e >> 8;
-        sd_pb[d] = (r ? 64u * seg[0] : 0u) + (e & 0xffu);
+        const uint32_t r = 4u * (uint32_t)d >= seg[0] ? 1u : 0u;
+        const uint32_t u = 4u * (uint32_t)d - (r ? seg[0] : 0u);
+        sd_pb[d] = (r ? 64u * seg[0] : 0u) + u;
         sd_mul[d] = r ? seg[1] : seg[0];
     }
 
@@ -380,6 +391,98 @@ __device__ __forceinline__ void decode_fast(uint32_t *misc, uint8_t *smem, const
     }
 }
 
+// Wave-parallel header parse (decode :271-304, deserialize :119-170, recombine :614-637) for
+// the blobs the fast path takes: UNCP, or a valid TDT blob with word size 1/2/4/8/16, at most
+// 16 streams, a mapping inside the header cache, at most two referenced streams whose
+// per-group segments are whole dwords, and wc > 0.  Anything else (errors included) returns
+// kind 0 and goes through the lane-0 parser (blob_check) and the generic path, which assign
+// the reference's status codes.  hdr: the blob's first 256 bytes (zero-padded) in LDS.
+__device__ __forceinline__ FastHdr parse_fast(const uint8_t *blob, uint64_t len, const uint8_t *hdr, uint32_t hcl) {
+    const uint32_t lane = (uint32_t)lane_id();
+    FastHdr h{};
+    h.kind = 0;
+    auto hw = [&](uint32_t off) -> uint32_t { return *reinterpret_cast<const uint32_t *>(hdr + off); };  // off % 4 == 0
+    if (len < 4) return h;
+    const uint32_t magic = hw(0);
+    if (magic == kMagicUNCP) {
+        h.kind = 1;
+        h.osize = len - 4;
+        return h;
+    }
+    if (magic != kMagicTDT || len < 20) return h;
+    const uint32_t orig = hw(4), ns = hw(8), ws = hw(12), msize = hw(16);
+    if (!(ws == 1 || ws == 2 || ws == 4 || ws == 8 || ws == 16) || msize < ws || ns == 0 || ns > 16) return h;
+    if (20u + 4u * msize + 4u > hcl || orig / ws == 0) return h;
+    // stream table: lane s keeps stream s's data offset and length
+    uint64_t off = 20ull + 4ull * msize;
+    uint32_t my_off = 0, my_len = 0;
+    for (uint32_t s = 0; s < ns; ++s) {  // uniform
+        if (off + 4 > len) return h;
+        const uint32_t l = off + 4 <= hcl ? ld_u32_bytes(hdr + off) : ld_u32_bytes(blob + off);
+        off += 4;
+        if (off + l > len) return h;
+        if (lane == s) {
+            my_off = (uint32_t)off;
+            my_len = l;
+        }
+        off += l;
+    }
+    // mapping: lane b < ws holds mapping[b]; k = how many positions share it, rank = how many
+    // before b, first = the lowest such position
+    const uint32_t m = lane < ws ? hw(20 + 4 * lane) : 0xffffffffu;
+    if (__any(lane < ws && m >= ns)) return h;  // (also negative values) → BAD_MAPPING via blob_check
+    uint32_t k = 0, rank = 0, first = lane;
+    for (uint32_t bb = 0; bb < ws; ++bb) {  // uniform
+        const uint32_t mb = (uint32_t)__builtin_amdgcn_readlane((int)m, (int)bb);
+        if (mb == m) {
+            ++k;
+            if (bb < lane) ++rank;
+            first = first < bb ? first : bb;
+        }
+    }
+    const uint64_t fum = __ballot(lane < ws && first == lane);  // first uses, in order
+    if (__builtin_popcountll(fum) > 2) return h;
+    const uint32_t f0 = (uint32_t)__builtin_ctzll(fum);
+    const uint64_t fum1 = fum & (fum - 1);
+    const bool two = fum1 != 0;
+    const uint32_t f1 = two ? (uint32_t)__builtin_ctzll(fum1) : f0;
+    const uint32_t WPG = 16 / ws;
+    const uint32_t seg0 = WPG * (uint32_t)__builtin_amdgcn_readlane((int)k, (int)f0);
+    const uint32_t seg1 = two ? WPG * (uint32_t)__builtin_amdgcn_readlane((int)k, (int)f1) : 0u;
+    if ((seg0 & 3u) || (seg1 & 3u)) return h;
+    const uint32_t m0 = (uint32_t)__builtin_amdgcn_readlane((int)m, (int)f0);
+    const uint32_t m1 = (uint32_t)__builtin_amdgcn_readlane((int)m, (int)f1);
+    h.soff[0] = (uint32_t)__builtin_amdgcn_readlane((int)my_off, (int)m0);
+    h.np[0] = (uint32_t)__builtin_amdgcn_readlane((int)my_len, (int)m0) / 2u;
+    h.soff[1] = two ? (uint32_t)__builtin_amdgcn_readlane((int)my_off, (int)m1) : 0u;
+    h.np[1] = two ? (uint32_t)__builtin_amdgcn_readlane((int)my_len, (int)m1) / 2u : 0u;
+    // recombine selectors: output byte i = word i / ws, position b = i % ws of stream
+    // r = ref(mapping[b]) → S byte (r ? seg0 : 0) + (i / ws)·k_b + rank_b
+    const uint32_t i = lane & 15u, b = i % ws;
+    const uint32_t kb = (uint32_t)__shfl((int)k, (int)b), rb = (uint32_t)__shfl((int)rank, (int)b);
+    const uint32_t fb = (uint32_t)__shfl((int)first, (int)b);
+    const uint32_t sidx = (fb == f0 ? 0u : seg0) + (i / ws) * kb + rb;
+    const uint32_t sh = 8u * (i & 3u);
+    uint32_t A = (sidx < 8u ? sidx : 0x0cu) << sh, B = (sidx >= 8u ? sidx - 8u : 0x0cu) << sh;
+    A |= dpp_mov_self<0xb1>(A);  // quad_perm [1,0,3,2]
+    A |= dpp_mov_self<0x4e>(A);  // quad_perm [2,3,0,1]
+    B |= dpp_mov_self<0xb1>(B);
+    B |= dpp_mov_self<0x4e>(B);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        h.OA[q] = (uint32_t)__builtin_amdgcn_readlane((int)A, 4 * q);
+        h.OB[q] = (uint32_t)__builtin_amdgcn_readlane((int)B, 4 * q);
+    }
+    h.orig = orig;
+    h.ws = ws;
+    h.two = two ? 1u : 0u;
+    h.seg[0] = seg0;
+    h.seg[1] = seg1;
+    h.osize = orig;
+    h.kind = 2;
+    return h;
+}
+
 template <int LB>
 __global__ __launch_bounds__(64) void tdt_decode_kernel(DecodeArgs a) {
     using Lay = DecLayout;
@@ -406,14 +509,55 @@ __global__ __launch_bounds__(64) void tdt_decode_kernel(DecodeArgs a) {
     // ------------------------------------------------ header cache: first 256 bytes in LDS
     {
         const uint64_t hc = len < (uint64_t)kHdrCache ? len : (uint64_t)kHdrCache;
+        const uint32_t o = (uint32_t)lane * 4u;
+        uint32_t w = 0;
+        if (((uintptr_t)blob & 3) == 0 && o + 4 <= hc) {
+            w = *reinterpret_cast<const uint32_t *>(blob + o);  // one dword per lane
+        } else {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const uint32_t o = (uint32_t)lane * 4u + (uint32_t)i;
-            hdrc[o] = o < hc ? blob[o] : (uint8_t)0;
+            for (int i = 0; i < 4; ++i)
+                if (o + i < hc) w |= (uint32_t)blob[o + i] << (8 * i);
         }
+        reinterpret_cast<uint32_t *>(hdrc)[lane] = w;
     }
     team_sync<1>();
     const uint32_t hcl = len < (uint64_t)kHdrCache ? (uint32_t)len : (uint32_t)kHdrCache;
+
+    // ------------------------------------------------ fast path (wave-parallel header parse)
+    const FastHdr H = parse_fast(blob, len, hdrc, hcl);
+    if (H.kind != 0) {
+        const uint64_t osize = H.osize;
+        uint64_t ob;
+        bool fits;
+        if constexpr (LB) {
+            ob = lookback_excl_wave(a.lookback, msg, osize, a.errflags);
+            fits = ob + osize <= a.out_cap;
+        } else {
+            ob = a.slot_off[msg];
+            fits = osize <= a.slot_off[msg + 1] - ob;
+        }
+        const uint32_t st = fits ? ST_OK : ST_CAPACITY;
+        if (lane == 0) {
+            if constexpr (LB) {
+                a.out_off[msg] = ob;
+                if (msg == a.n_msgs - 1) a.out_off[a.n_msgs] = ob + osize;
+            } else {
+                if (a.out_len) a.out_len[msg] = fits ? osize : 0;
+            }
+            if (a.status) a.status[msg] = (int32_t)st;
+        }
+        if (!fits) return;
+        uint8_t *dst = a.out + ob;
+        if (H.kind == 1) {
+            team_copy_g2g<64>(dst, blob + 4, len - 4);
+            return;
+        }
+        const uint64_t wbytes = (uint64_t)(H.orig / H.ws) * H.ws;
+        // recombine :617 zero-initialises; bytes past the last whole word stay zero
+        if (H.orig > wbytes) team_zero<64>(dst + wbytes, H.orig - wbytes);
+        decode_fast(H, smem, blob, blim, dst, (uint32_t)((wbytes + 15) / 16), wbytes);
+        return;
+    }
     auto rd32 = [&](uint64_t off) -> uint32_t {
         if (off + 4 <= hcl) {
             if ((off & 3) == 0) return *reinterpret_cast<const uint32_t *>(hdrc + off);
@@ -551,10 +695,7 @@ __global__ __launch_bounds__(64) void tdt_decode_kernel(DecodeArgs a) {
     uint16_t *heads = reinterpret_cast<uint16_t *>(smem + Lay::OFF_HEADS);
     uint8_t *planes = smem + Lay::OFF_PLANES;
 
-    if (fast && nref <= 2) {
-        decode_fast(misc, smem, blob, blim, dst, ngroups, wbytes, WPG, nref, OA, OB);
-        return;
-    }
+    // (blobs parse_fast accepts never get here; the generic path serves every other shape)
 
     // ---------------------------------------------------------------- generic path
     // (more than two referenced streams, or stream segments that are not whole dwords)
