@@ -70,6 +70,9 @@ class Oracle:
         L.tdt_oracle_decode.argtypes = [_u8p, C.c_uint64, _u8p, C.c_uint64, _u64p]
         L.tdt_oracle_decoded_size.restype = C.c_int
         L.tdt_oracle_decoded_size.argtypes = [_u8p, C.c_uint64, _u64p]
+        L.tdt_oracle_encode_batch_mt.restype = C.c_int
+        L.tdt_oracle_encode_batch_mt.argtypes = [_u8p, _u64p, C.c_uint32, C.POINTER(OracleConfig), C.c_double,
+                                                 C.c_double, _u8p, _u64p, _u64p, _i32p, C.c_int]
 
     @staticmethod
     def config(word_size=4, sample_fraction=1.0, bandwidth_threshold_mbps=100.0,
@@ -127,6 +130,29 @@ class Oracle:
         return st, out[: olen.value].tobytes() if st == 0 else b""
 
     # batch conveniences -------------------------------------------------------------
+    def encode_slotted(self, data: np.ndarray, offsets: np.ndarray, cfg=None, bandwidth=10.0, cpu=0.5,
+                       threads: int = 0):
+        """Encode every message into its own slot (slot i = the prefix of tdt_encode_bound),
+        on `threads` host threads (0 = all usable cores).  Returns (out, slot_off, lengths)."""
+        cfg = cfg or self.config()
+        d = np.ascontiguousarray(data, dtype=np.uint8).reshape(-1)
+        off = np.ascontiguousarray(offsets, dtype=np.uint64)
+        n = off.size - 1
+        sizes = np.diff(off.astype(np.int64))
+        bounds = np.maximum(sizes + 4, 20 + 4 * cfg.word_size + 8 + 2 * sizes)
+        slot = np.zeros(n + 1, np.uint64)
+        np.cumsum(bounds, out=slot[1:])
+        out = np.empty(max(int(slot[-1]), 1), np.uint8)
+        lens = np.zeros(max(n, 1), np.uint64)
+        st = np.zeros(max(n, 1), np.int32)
+        thr = threads or len(os.sched_getaffinity(0))
+        r = self.lib.tdt_oracle_encode_batch_mt(_ptr(d) if d.size else _ptr(np.zeros(1, np.uint8)), _ptr(off, _u64p),
+                                                n, C.byref(cfg), bandwidth, cpu, _ptr(out), _ptr(slot, _u64p),
+                                                _ptr(lens, _u64p), _ptr(st, _i32p), int(thr))
+        if r:
+            raise ValueError("oracle batch encode: status %d" % int(st[st != 0][0]))
+        return out, slot, lens[:n]
+
     def encode_batch(self, data: np.ndarray, offsets: np.ndarray, **kw) -> tuple[bytes, np.ndarray]:
         """Encode every message; returns (concatenated blobs, blob offsets[n+1])."""
         blobs = [self.encode(data[offsets[i]:offsets[i + 1]], **kw) for i in range(len(offsets) - 1)]
@@ -152,6 +178,9 @@ class Reference:
         L.tdt_ref_last_error.restype = C.c_char_p
         L.tdt_ref_should_transform.restype = C.c_int
         L.tdt_ref_should_transform.argtypes = [_u8p, C.c_size_t, C.c_int, C.c_double, C.c_double, C.c_size_t]
+        L.tdt_ref_encode_ratio.restype = C.c_int
+        L.tdt_ref_encode_ratio.argtypes = [_u8p, C.c_size_t, C.c_float, C.c_int, C.c_double,
+                                           C.POINTER(C.c_double), C.POINTER(C.c_int)]
         L.tdt_ref_bench.restype = C.c_double
         L.tdt_ref_bench.argtypes = [_u8p, _u64p, C.c_uint32, C.c_float, C.c_int, C.c_int, C.c_int, _u64p]
 
@@ -181,6 +210,15 @@ class Reference:
         st = self.lib.tdt_ref_decode(bp, b.size, _ptr(out), cap, C.byref(olen))
         err = self.lib.tdt_ref_last_error().decode() if st == -1 else ""
         return st, out[: olen.value].tobytes() if st == 0 else b"", err
+
+    def encode_ratio(self, data, sample_fraction=1.0, word_size=4, bandwidth=10.0):
+        """(blob length, transformation_ratio(), processing_overhead_ms() changed?) after one encode."""
+        d = _bytes(data)
+        ratio, upd = C.c_double(0.0), C.c_int(0)
+        dp = _ptr(d) if d.size else _ptr(np.zeros(1, np.uint8))
+        n = self.lib.tdt_ref_encode_ratio(dp, d.size, sample_fraction, word_size, bandwidth, C.byref(ratio),
+                                          C.byref(upd))
+        return n, ratio.value, bool(upd.value)
 
     def should_transform(self, n, word_size=4, bandwidth=10.0, cpu=0.5, min_tensor_size=1024) -> bool:
         d = np.zeros(max(n, 1), np.uint8)

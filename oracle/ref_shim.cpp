@@ -57,6 +57,20 @@ int tdt_ref_encode(const uint8_t *data, size_t n, float sample_fraction, int wor
     return 0;
 }
 
+// Encode one message and report the reference's own transformation_ratio() (:329-331, set by
+// compress_tdt :395-396 from encoded_size() :71-78) and whether processing_overhead_ms()
+// (:332-334) changed (it does only on the compress path).
+int tdt_ref_encode_ratio(const uint8_t *data, size_t n, float sample_fraction, int word_size,
+                         double bandwidth_mbps, double *ratio, int *overhead_updated) {
+    TDTCompressionProtocol p(make_cfg(sample_fraction, word_size, 1024));
+    p.update_network_metrics(bandwidth_mbps, 1.0);
+    const double before = p.processing_overhead_ms();
+    std::vector<uint8_t> blob = p.encode(const_cast<uint8_t *>(data), n);
+    *ratio = p.transformation_ratio();
+    *overhead_updated = p.processing_overhead_ms() != before ? 1 : 0;
+    return (int)blob.size();
+}
+
 int tdt_ref_should_transform(const uint8_t *data, size_t n, int word_size,
                              double bandwidth_mbps, double cpu_usage,
                              size_t min_tensor_size) {

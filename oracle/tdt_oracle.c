@@ -11,6 +11,7 @@
 #include "tdt_oracle.h"
 
 #include <math.h>
+#include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -319,4 +320,47 @@ int tdt_oracle_decode_batch(const uint8_t *in, const uint64_t *in_off, uint32_t 
         any |= status[i];
     }
     return any ? 1 : 0;
+}
+
+/* Threaded batch encode into caller slots (tests of 10^5..10^6 messages): `threads` workers,
+ * message i on worker i % threads.  Same per-message semantics as tdt_oracle_encode_batch. */
+typedef struct {
+    const uint8_t *in;
+    const uint64_t *in_off;
+    uint32_t n_msgs, t, threads;
+    const tdt_oracle_config *cfg;
+    double bw, cpu;
+    uint8_t *out;
+    const uint64_t *slot_off;
+    uint64_t *out_len;
+    int32_t *status;
+} enc_job;
+
+static void *enc_worker(void *arg) {
+    enc_job *j = (enc_job *)arg;
+    for (uint32_t i = j->t; i < j->n_msgs; i += j->threads)
+        j->status[i] = tdt_oracle_encode(j->in + j->in_off[i], j->in_off[i + 1] - j->in_off[i], j->cfg, j->bw,
+                                         j->cpu, NULL, j->out + j->slot_off[i],
+                                         j->slot_off[i + 1] - j->slot_off[i], &j->out_len[i]);
+    return NULL;
+}
+
+int tdt_oracle_encode_batch_mt(const uint8_t *in, const uint64_t *in_off, uint32_t n_msgs,
+                               const tdt_oracle_config *cfg, double bandwidth_mbps, double cpu_usage,
+                               uint8_t *out, const uint64_t *slot_off, uint64_t *out_len, int32_t *status,
+                               int threads) {
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    pthread_t tid[256];
+    enc_job jobs[256];
+    for (int t = 0; t < threads; ++t) {
+        enc_job j = {in, in_off, n_msgs, (uint32_t)t, (uint32_t)threads, cfg, bandwidth_mbps, cpu_usage,
+                     out, slot_off, out_len, status};
+        jobs[t] = j;
+        pthread_create(&tid[t], NULL, enc_worker, &jobs[t]);
+    }
+    for (int t = 0; t < threads; ++t) pthread_join(tid[t], NULL);
+    for (uint32_t i = 0; i < n_msgs; ++i)
+        if (status[i]) return 1;
+    return 0;
 }

@@ -73,6 +73,10 @@ int tdt_oracle_encode_batch(const uint8_t *in, const uint64_t *in_off, uint32_t 
                             const tdt_oracle_config *cfg, double bandwidth_mbps,
                             double cpu_usage, uint8_t *out, const uint64_t *slot_off,
                             uint64_t *out_len, int32_t *status);
+int tdt_oracle_encode_batch_mt(const uint8_t *in, const uint64_t *in_off, uint32_t n_msgs,
+                               const tdt_oracle_config *cfg, double bandwidth_mbps,
+                               double cpu_usage, uint8_t *out, const uint64_t *slot_off,
+                               uint64_t *out_len, int32_t *status, int threads);
 int tdt_oracle_decode_batch(const uint8_t *in, const uint64_t *in_off, uint32_t n_msgs,
                             uint8_t *out, const uint64_t *slot_off, uint64_t *out_len,
                             int32_t *status);

@@ -53,6 +53,20 @@ class TDTConfig:
                           self.cpu_usage_threshold, self.min_tensor_size)
 
 
+def transformation_ratio_of(blob: bytes, n: int) -> float | None:
+    """The reference's transformation_ratio() after encoding n bytes into `blob`
+    (compress_tdt :395-396): n / TDTEncodedData::encoded_size() (:71-78), which counts the RLE
+    stream bytes, the mapping ints and sizeof(TDTEncodedData) = 72 (x86-64 libstdc++: two
+    vectors, size_t, int, double) — not the serialized length.  None for a UNCP blob (the
+    reference leaves the ratio unchanged on the passthrough path, :230-236 and :256-265)."""
+    if len(blob) < 20 or int.from_bytes(blob[:4], "little") != MAGIC_TDT:
+        return None
+    ns = int.from_bytes(blob[8:12], "little")
+    msize = int.from_bytes(blob[16:20], "little")
+    streams = len(blob) - 20 - 4 * msize - 4 * ns
+    return float(n) / float(streams + 4 * msize + 72)
+
+
 def encode_bound(n: int, word_size: int = 4) -> int:
     return int(_lib.load().tdt_encode_bound(n, word_size))
 
@@ -313,11 +327,9 @@ class TDTCompressionProtocol:
         if int(st[0]) != 0:
             raise TdtError(int(st[0]), "encode")
         blob = out.tobytes()
-        if int.from_bytes(blob[:4], "little") == MAGIC_TDT:
-            ns = int.from_bytes(blob[8:12], "little")
-            # encoded_size() counts sizeof(TDTEncodedData) = 72 and the mapping ints (:71-78)
-            enc_size = (len(blob) - 20 - 4 * self.config_.word_size - 4 * ns) + 4 * self.config_.word_size + 72
-            self.last_compression_ratio_ = n / enc_size
+        ratio = transformation_ratio_of(blob, n)
+        if ratio is not None:  # compressed: metrics as :243-248
+            self.last_compression_ratio_ = ratio
             self.last_encode_time_ms_ = (time.perf_counter() - t0) * 1e3
         return blob
 

@@ -81,3 +81,38 @@ extern "C" int selftest_run(const uint32_t *d_in, uint32_t *d_out) {
     hipLaunchKernelGGL(selftest_kernel, dim3(1), dim3(256), 0, 0, d_in, d_out);
     return hipDeviceSynchronize() == hipSuccess ? 0 : 1;
 }
+
+// ---------------------------------------------------------------------------------------
+// Entropy arithmetic on the device, exactly as tdt_encode_kernel evaluates it (SURVEY.md §7
+// hard part (i)): for c = 1..N, prob = (double)c / N, L = psy_log2_glibc(prob) with the
+// glibc tables staged in LDS, and the entropy step fma(-prob, L, 0.0).  out: 2N doubles
+// (L, step) per c.  The test compares them bitwise with the host's libm.
+#include "../../psyne_amd/csrc/tdt_log2.h"
+
+__constant__ __attribute__((aligned(16))) double st_log2_tab[128] = PSY_LOG2_TAB_INIT;
+__constant__ __attribute__((aligned(16))) double st_log2_tab2[128] = PSY_LOG2_TAB2_INIT;
+
+__global__ __launch_bounds__(256) void log2_sweep_kernel(uint32_t N, double *out) {
+    __shared__ double tab[256];
+    for (int i = threadIdx.x; i < 128; i += 256) {
+        tab[i] = st_log2_tab[i];
+        tab[128 + i] = st_log2_tab2[i];
+    }
+    __syncthreads();
+    const uint32_t c = blockIdx.x * 256u + threadIdx.x + 1u;
+    if (c > N) return;
+    double prob, L;
+    {
+#pragma clang fp contract(off)
+        prob = (double)c / (double)N;
+        L = psy_log2_glibc(prob, tab, tab + 128);
+    }
+    out[2ull * (c - 1)] = L;
+    out[2ull * (c - 1) + 1] = __builtin_fma(-prob, L, 0.0);
+}
+
+extern "C" int selftest_log2_sweep(uint32_t N, double *d_out) {
+    if (N == 0) return 0;
+    hipLaunchKernelGGL(log2_sweep_kernel, dim3((N + 255) / 256), dim3(256), 0, 0, N, d_out);
+    return hipDeviceSynchronize() == hipSuccess ? 0 : 1;
+}

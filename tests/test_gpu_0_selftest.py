@@ -89,3 +89,26 @@ def test_unaligned_lds():
     words = np.frombuffer(bytes(buf), np.uint32)
     x = np.array([words[l] ^ words[l + 1] ^ words[l + 2] ^ words[l + 3] for l in range(64)], np.uint32)
     assert np.array_equal(o[64:128], x), "ds_read_b128 at 4-byte alignment"
+
+
+@pytest.mark.parametrize("N", [256, 16384, 262144])
+def test_device_log2_sweep(N):
+    """Every c/N the entropy pass can form for a message of N words (1 KiB, 64 KiB and 1 MiB
+    float32 messages): the device's restated glibc log2 and entropy step fma(-p, log2 p, 0)
+    are bit-identical to this host's libm log2 (SURVEY.md §7 hard part (i))."""
+    import ctypes.util
+    lib = C.CDLL(str(LIB))
+    lib.selftest_log2_sweep.argtypes = [C.c_uint32, C.c_void_p]
+    out = torch.zeros(2 * N, dtype=torch.float64, device="cuda")
+    assert lib.selftest_log2_sweep(N, C.c_void_p(out.data_ptr())) == 0
+    got = out.cpu().numpy().reshape(N, 2)
+    libm = C.CDLL(ctypes.util.find_library("m"))
+    libm.log2.restype = C.c_double
+    libm.log2.argtypes = [C.c_double]
+    p = np.arange(1, N + 1, dtype=np.float64) / np.float64(N)
+    want_l = np.array([libm.log2(float(x)) for x in p])
+    assert np.array_equal(got[:, 0].view(np.uint64), want_l.view(np.uint64)), "device log2 != libm log2"
+    # fma(-p, L, 0.0) rounds the exact product once and adds +0.0 (so -0.0 becomes +0.0): the
+    # same as a rounded double multiply followed by + 0.0
+    want_s = (-p) * want_l + 0.0
+    assert np.array_equal(got[:, 1].view(np.uint64), want_s.view(np.uint64)), "entropy step"

@@ -1,0 +1,123 @@
+"""GPU parity at BASELINE sizes: the HIP codec through the C ABI against
+the C oracle (pinned by tests/golden/) on the full C2 batch, on 100 k mixed messages, and on
+single messages up to SimpleTCP's 100 MB frame cap (tcp_simple.hpp:127-134) at several
+alignments.  Bit-exact: byte/integer work with a bit-exact restated entropy decision."""
+import numpy as np
+import pytest
+
+from oracle.oracle import Oracle
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+
+
+def make_codec():
+    from psyne_amd import TDTConfig, TdtCodec
+    c = TdtCodec(TDTConfig(sample_fraction=1.0))
+    c.set_metrics(10.0, 1.0, 0.5)  # bandwidth < 100 Mbps: compression on
+    return c
+
+
+def valid_mask(slot, lens, total):
+    """Bytes [slot[i], slot[i] + lens[i]) of a slotted buffer of `total` bytes."""
+    d = np.zeros(total + 1, np.int32)
+    np.add.at(d, slot[:-1].astype(np.int64), 1)
+    np.add.at(d, (slot[:-1] + lens).astype(np.int64), -1)
+    return np.cumsum(d[:-1]) > 0
+
+
+def check_slotted(codec, data, off, chunk=131072):
+    """Encode the batch on the GPU into slots, compare every blob with the oracle (threaded,
+    chunked), then decode the GPU blobs back and compare with the input on the device."""
+    orc = Oracle()
+    n = off.numel() - 1
+    out, slots, lens, st = codec.encode_into(data, off)
+    torch.cuda.synchronize()
+    assert int(st[:n].abs().sum()) == 0
+    offh = off.cpu().numpy().astype(np.uint64)
+    for c0 in range(0, n, chunk):
+        c1 = min(n, c0 + chunk)
+        a, b = int(offh[c0]), int(offh[c1])
+        host = data[a:b].cpu().numpy()
+        want, wslot, wlen = orc.encode_slotted(host, offh[c0:c1 + 1] - offh[c0], bandwidth=10.0)
+        glen = lens[c0:c1].cpu().numpy().astype(np.uint64)
+        assert np.array_equal(glen, wlen), "blob lengths differ in chunk %d" % c0
+        s0, s1 = int(slots[c0].item()), int(slots[c1].item())
+        got = out[s0:s1].cpu().numpy()
+        gslot = slots[c0:c1 + 1].cpu().numpy().astype(np.uint64) - np.uint64(s0)
+        assert np.array_equal(gslot, wslot), "slot layout differs"
+        m = valid_mask(wslot, wlen, int(wslot[-1]))
+        assert np.array_equal(got[m], want[: m.size][m]), "blob bytes differ in chunk %d" % c0
+    back, dsl, dln, dst = codec.decode_into(out, slots, in_lengths=lens)
+    torch.cuda.synchronize()
+    assert int(dst[:n].abs().sum()) == 0
+    assert torch.equal(back[: int(offh[-1] - offh[0])], data[int(offh[0]):int(offh[-1])])
+
+
+@pytest.mark.timeout(600)
+def test_c2_full_batch_bitexact():
+    """BASELINE configs[1] as bench.py --workload c2 runs it: 1,048,576 x 1 KiB uniform random
+    payloads generated on the device (seed 0x5EED0001), every blob compared with the oracle."""
+    import bench
+    n = 1 << 20
+    data = bench.gen_uniform(torch, n * 1024, 0x5EED0001, torch.device("cuda"))
+    off = torch.arange(n + 1, dtype=torch.int64, device="cuda") * 1024
+    check_slotted(make_codec(), data, off)
+
+
+@pytest.mark.timeout(300)
+def test_100k_mixed_vs_oracle():
+    """100,000 messages of 64 B - 8 KiB (UNCP below 1 KiB), half uniform bytes, half
+    gradient-like float32, every blob compared with the oracle."""
+    rng = np.random.default_rng(51)
+    n = 100_000
+    sizes = rng.integers(1, 129, n) * 64
+    off = np.zeros(n + 1, np.int64)
+    off[1:] = np.cumsum(sizes)
+    buf = rng.integers(0, 256, int(off[-1]), dtype=np.uint8)
+    for i in range(0, n, 2):  # gradient-like content in every other message
+        k = int(sizes[i]) // 4
+        x = rng.normal(0, 0.01, k).astype(np.float32)
+        x[rng.random(k) < 0.7] = 0
+        buf[off[i]:off[i + 1]] = x.view(np.uint8)
+    check_slotted(make_codec(), torch.from_numpy(buf).cuda(), torch.from_numpy(off).cuda())
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("n,lead", [(16 << 20, 0), (16 << 20, 1), (16 << 20, 3), (16 << 20, 8),
+                                    (100 * 1024 * 1024, 0), (100 * 1024 * 1024, 3)])
+def test_large_message(n, lead):
+    """One message of 16 MiB or 100 MB (SimpleTCP's frame cap, tcp_simple.hpp:127-134) at a
+    misaligned start, between two small neighbours: compacted encode (look-back) and decode."""
+    rng = np.random.default_rng(n % 1000 + lead)
+    k = n // 4
+    x = rng.normal(0, 0.01, k).astype(np.float32)
+    x[rng.random(k) < 0.7] = 0
+    big = x.view(np.uint8)
+    small = [rng.integers(0, 256, 4096, dtype=np.uint8), rng.integers(0, 4, 2048, dtype=np.uint8)]
+    msgs = [small[0], big, small[1]]
+    off = np.zeros(4, np.int64)
+    off[0] = lead
+    for i, m in enumerate(msgs):
+        off[i + 1] = off[i] + m.size
+    buf = np.zeros(int(off[-1]), np.uint8)
+    for i, m in enumerate(msgs):
+        buf[off[i]:off[i + 1]] = m
+    codec = make_codec()
+    d, o = torch.from_numpy(buf).cuda(), torch.from_numpy(off).cuda()
+    enc, eoff, st = codec.encode_batch(d, o)
+    torch.cuda.synchronize()
+    assert int(st[:3].abs().sum()) == 0
+    e, eo = enc.cpu().numpy(), eoff.cpu().numpy()
+    orc = Oracle()
+    for i, m in enumerate(msgs):
+        assert e[eo[i]:eo[i + 1]].tobytes() == orc.encode(m, bandwidth=10.0), "message %d" % i
+    dec, doff, dst = codec.decode_batch(enc, eoff)
+    torch.cuda.synchronize()
+    assert int(dst[:3].abs().sum()) == 0
+    assert torch.equal(dec[: int(off[-1] - off[0])], d[int(off[0]):])
