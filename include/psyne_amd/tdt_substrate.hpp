@@ -2,20 +2,28 @@
 //
 // psyne's network substrate (reference include/psyne/channel/substrate/tcp_simple.hpp) frames
 // every message as a u32 length followed by the payload (transport_send :68-91,
-// transport_receive :96-150, try_transport_receive :153-194).  docs/tdt_attribution.md:62-75
+// transport_receive :96-150, try_transport_receive :153-194); docs/tdt_attribution.md:62-75
 // describes the intended TDT-over-IP substrate: payloads compressed before the socket and
 // restored after it.  This header provides both halves for an MI355X host:
 //
-//   * PosixTcpSubstrate — SimpleTCP's SubstrateBehavior surface (allocate/deallocate slab,
+//   * PosixTcpSubstrate — SimpleTCP's public surface (allocate/deallocate slab,
 //     transport_send/receive, try_transport_receive, identity, statistics, wait_for_connection)
-//     over blocking POSIX sockets (the image has no Boost.Asio), byte-identical framing and
-//     the reference's error texts.
-//   * TdtSubstrate<Inner> — a decorator over any substrate with that surface: transport_send
-//     encodes the payload with the GPU codec (HipTDTCompressionProtocol: UNCP passthrough when
-//     the policy says so, exactly like the reference codec) and sends the blob through Inner's
-//     framing; transport_receive takes one frame from Inner and decodes it.  send_batch /
-//     receive_batch move many messages per GPU call through the C ABI host pipeline
-//     (tdt_encode_host / tdt_decode_host: chunked, H2D / kernel / D2H overlapped on two
+//     over blocking POSIX sockets (the image has no Boost.Asio): byte-identical framing and the
+//     reference's error texts.  Nothing beyond SimpleTCP's method set.
+//   * TdtSubstrate<Inner, Base> — a substrate in the shape of psyne's SubstrateBehavior
+//     (core/behaviors.hpp:32-48) that decorates any Inner with SimpleTCP's surface: it OWNS the
+//     inner substrate and a GPU codec (HipTDTCompressionProtocol), is default-constructible as
+//     ChannelBridge requires (behaviors.hpp:150: std::make_unique<SubstrateType>()),
+//     transport_send encodes and sends one frame, transport_receive(void*, size_t) blocks until
+//     one frame has arrived and decodes it into the buffer.  Frame lengths come from Inner's
+//     try_transport_receive(buf, cap, received_size) (tcp_simple.hpp:153-194) — the only
+//     receive that reports a length.  A frame is checked against the buffer BEFORE decoding:
+//     its header's decoded size (UNCP: len - 4, TDT: original_size) must fit, so a crafted
+//     header cannot make the receiver allocate or decode beyond buffer_size.
+//     Base: the vtable to implement — psyne::behaviors::SubstrateBehavior in a psyne build
+//     (every method here matches its signature, so it overrides), an empty struct otherwise.
+//     send_batch / receive_batch move many messages per GPU call through the C ABI host
+//     pipeline (tdt_encode_host / tdt_decode_host: chunked, H2D / kernel / D2H overlapped on two
 //     streams), which is how the codec reaches PCIe rates instead of per-message latency.
 #pragma once
 
@@ -38,6 +46,7 @@
 #include <stdexcept>
 #include <string>
 #include <thread>
+#include <utility>
 #include <vector>
 
 namespace psyne_amd {
@@ -45,7 +54,7 @@ namespace psyne_amd {
 class PosixTcpSubstrate {
 public:
     // host: bind address (server) or remote host (client); as SimpleTCP(host, port, is_server)
-    explicit PosixTcpSubstrate(const std::string &host = "127.0.0.1", uint16_t port = 8080, bool is_server = false)
+    explicit PosixTcpSubstrate(const std::string &host = "localhost", uint16_t port = 8080, bool is_server = false)
         : host_(host), port_(port), is_server_(is_server) {
         if (is_server_) {
             listen_fd_ = ::socket(AF_INET, SOCK_STREAM, 0);
@@ -108,7 +117,7 @@ public:
         packets_sent_++;
     }
 
-    // (:96-150) one frame into buffer; its size is last_received_size()
+    // (:96-150) one frame into buffer (the caller learns no length: SubstrateBehavior's shape)
     void transport_receive(void *buffer, size_t buffer_size) {
         if (!is_connected()) throw std::runtime_error("TCP: Not connected");
         std::lock_guard<std::mutex> lk(mu_);
@@ -125,12 +134,13 @@ public:
             throw std::runtime_error("TCP receive failed: TCP: Suspicious message size detected");
         }
         if (!read_all(buffer, hdr)) fail("TCP receive failed: connection lost");
-        last_received_ = hdr;
         bytes_received_ += hdr + sizeof(hdr);
         packets_received_++;
     }
 
-    // (:153-194) non-blocking probe: a frame is read only when its length word has arrived
+    // (:153-194) non-blocking probe: a frame is read only when its length word has arrived;
+    // like SimpleTCP it never throws (an oversized frame or a failed read drops the connection
+    // and returns false)
     bool try_transport_receive(void *buffer, size_t buffer_size, size_t &received_size) {
         if (!is_connected()) return false;
         std::lock_guard<std::mutex> lk(mu_);
@@ -138,10 +148,12 @@ public:
         const ssize_t got = ::recv(fd_, &hdr, sizeof(hdr), MSG_PEEK | MSG_DONTWAIT);
         if (got < (ssize_t)sizeof(hdr)) return false;
         if (!read_all(&hdr, sizeof(hdr))) return fail_quiet();
-        if (hdr > buffer_size) throw std::runtime_error("TCP: Received message too large for buffer");
+        if (hdr > buffer_size) {  // "TCP: Received message too large for buffer", caught :189-191
+            close_socket();
+            return false;
+        }
         if (!read_all(buffer, hdr)) return fail_quiet();
         received_size = hdr;
-        last_received_ = hdr;
         bytes_received_ += hdr + sizeof(hdr);
         packets_received_++;
         return true;
@@ -163,13 +175,12 @@ public:
     size_t get_bytes_received() const { return bytes_received_; }
     size_t get_packets_sent() const { return packets_sent_; }
     size_t get_packets_received() const { return packets_received_; }
-    size_t last_received_size() const { return last_received_; }
     const std::string &get_host() const { return host_; }
     uint16_t get_port() const { return port_; }
     bool is_server_mode() const { return is_server_; }
 
 private:
-    static constexpr size_t kMaxReasonable = 100ull * 1024 * 1024;  // :132-140
+    static constexpr size_t kMaxReasonable = 100ull * 1024 * 1024;  // :127-134
 
     void adopt(int fd) {
         int one = 1;
@@ -231,21 +242,63 @@ private:
     std::thread accept_thread_, connect_thread_;
     std::atomic<bool> connected_{false}, stop_{false};
     std::mutex mu_;
-    size_t slab_size_ = 0, last_received_ = 0;
+    size_t slab_size_ = 0;
     size_t bytes_sent_ = 0, bytes_received_ = 0, packets_sent_ = 0, packets_received_ = 0;
 };
 
-// Decorator: TDT payload compression on the GPU between the channel and a framed substrate.
-template <class Inner>
-class TdtSubstrate {
-public:
-    TdtSubstrate(Inner &inner, HipTDTCompressionProtocol &codec) : inner_(inner), codec_(codec) {}
+// Decoded size a blob's header claims (decode :271-304): UNCP → len - 4, TDT → original_size;
+// -1 when the header is unreadable (the decode then reports the reference's error).
+inline int64_t tdt_claimed_size(const uint8_t *blob, size_t len) {
+    if (len < 4) return -1;
+    uint32_t magic;
+    std::memcpy(&magic, blob, 4);
+    if (magic == 0x554E4350u) return (int64_t)len - 4;
+    if (magic != 0x54445444u || len < 8) return -1;
+    uint32_t orig;
+    std::memcpy(&orig, blob + 4, 4);
+    return (int64_t)orig;
+}
 
+struct NoSubstrateBase {};
+
+// Decorator: TDT payload compression on the GPU between the channel and a framed substrate.
+template <class Inner, class Base = NoSubstrateBase>
+class TdtSubstrate : public Base {
+public:
+    // Codec configuration of default-constructed decorators (ChannelBridge builds its substrate
+    // with `std::make_unique<SubstrateType>()`); the reference's own defaults otherwise
+    // (bandwidth 100 Mbps = passthrough, tdt_compression.hpp:39-40, :352).
+    struct Defaults {
+        TDTConfig config{};
+        double bandwidth_mbps = 100.0;
+        double latency_ms = 1.0;
+        int device = 0;
+    };
+    static Defaults &defaults() {
+        static Defaults d;
+        return d;
+    }
+
+    TdtSubstrate() : TdtSubstrate(defaults().config) {}
+    // inner_args: Inner's constructor arguments (SimpleTCP(host, port, is_server))
+    template <class... InnerArgs>
+    explicit TdtSubstrate(const TDTConfig &cfg, InnerArgs &&...inner_args)
+        : inner_(std::forward<InnerArgs>(inner_args)...), codec_(cfg, defaults().device) {
+        codec_.update_network_metrics(defaults().bandwidth_mbps, defaults().latency_ms);
+        name_ = std::string("TDT+") + inner_.substrate_name();
+    }
+    TdtSubstrate(const TdtSubstrate &) = delete;
+    TdtSubstrate &operator=(const TdtSubstrate &) = delete;
+
+    Inner &inner() { return inner_; }
+    HipTDTCompressionProtocol &codec() { return codec_; }
+
+    // MEMORY OWNERSHIP
     void *allocate_memory_slab(size_t n) { return inner_.allocate_memory_slab(n); }
     void deallocate_memory_slab(void *p) { inner_.deallocate_memory_slab(p); }
 
-    // One message: encode (UNCP when the policy is off, as TDTCompressionProtocol::encode
-    // :227-266) and send the blob as one frame.
+    // TRANSPORT: one message = one frame (UNCP when the policy is off, exactly as
+    // TDTCompressionProtocol::encode :227-266)
     void transport_send(void *data, size_t size) {
         std::vector<uint8_t> blob = codec_.encode(data, size);
         inner_.transport_send(blob.data(), blob.size());
@@ -253,17 +306,51 @@ public:
         wire_sent_ += blob.size();
     }
 
-    // One frame → decode → buffer; returns the decoded size (the reference throws on a
-    // malformed blob: decode :271-304).
-    size_t transport_receive(void *buffer, size_t buffer_size) {
-        stage_.resize(tdt_encode_bound(buffer_size, 4) + 64);
-        inner_.transport_receive(stage_.data(), stage_.size());
-        std::vector<uint8_t> blob(stage_.begin(), stage_.begin() + (ptrdiff_t)inner_.last_received_size());
-        std::vector<uint8_t> out = codec_.decode(blob);
-        if (out.size() > buffer_size) throw std::runtime_error("TDT: decoded message larger than the buffer");
-        std::memcpy(buffer, out.data(), out.size());
-        return out.size();
+    // Blocks until one frame has arrived, decodes it into buffer (its decoded size:
+    // last_received_size()).  Throws the reference's decode errors (:274-276, :127-129), the
+    // inner substrate's "TCP: Not connected", or "TDT: decoded message larger than the buffer".
+    void transport_receive(void *buffer, size_t buffer_size) {
+        size_t got = 0;
+        auto pause = std::chrono::microseconds(1);
+        while (!try_transport_receive(buffer, buffer_size, got)) {
+            if constexpr (requires(Inner &s) { s.is_connected(); }) {
+                if (!inner_.is_connected()) throw std::runtime_error("TCP: Not connected");
+            }
+            std::this_thread::sleep_for(pause);
+            if (pause < std::chrono::microseconds(200)) pause *= 2;
+        }
     }
+
+    // (tcp_simple.hpp:153-194 shape) false when no frame is waiting; otherwise one frame is
+    // taken from Inner, checked, decoded into buffer, and its decoded size returned.
+    bool try_transport_receive(void *buffer, size_t buffer_size, size_t &received_size) {
+        stage_.resize(frame_capacity(buffer_size));
+        size_t flen = 0;
+        if (!inner_.try_transport_receive(stage_.data(), stage_.size(), flen)) return false;
+        const int64_t claimed = tdt_claimed_size(stage_.data(), flen);
+        if (claimed > (int64_t)buffer_size) throw std::runtime_error("TDT: decoded message larger than the buffer");
+        // decode straight into the caller's buffer (GPU, C-ABI host path); no allocation sized by the frame
+        const uint64_t off[2] = {0, flen};
+        uint64_t ooff[2] = {0, 0};
+        int32_t st = 0;
+        if (tdt_decode_host(codec_.context(), stage_.data(), off, 1, static_cast<uint8_t *>(buffer), buffer_size,
+                            ooff, &st) != TDT_OK)
+            throw std::runtime_error(std::string("TDT: GPU decode failed: ") + tdt_last_error());
+        if (st != TDT_OK) throw std::runtime_error(tdt_status_string(st));
+        received_size = ooff[1];
+        last_received_ = received_size;
+        return true;
+    }
+
+    // SUBSTRATE IDENTITY
+    const char *substrate_name() const { return name_.c_str(); }
+    bool is_zero_copy() const { return false; }
+    bool is_cross_process() const { return inner_.is_cross_process(); }
+
+    // EXTENSIONS ----------------------------------------------------------------------------
+    size_t last_received_size() const { return last_received_; }
+    // wire bytes / payload bytes sent so far
+    double wire_ratio() const { return raw_sent_ ? double(wire_sent_) / double(raw_sent_) : 1.0; }
 
     // Many messages per GPU call: pack → tdt_encode_host (one pipelined batch) → one frame per
     // blob, in order.  Returns the wire bytes.
@@ -276,7 +363,8 @@ public:
         uint64_t cap = 0;
         for (size_t i = 0; i < n; ++i) cap += tdt_encode_bound(sizes[i], codec_.word_size());
         enc_.resize(cap);
-        std::vector<uint64_t> eoff(n + 1);
+        std::vector<uint64_t> &eoff = eoff_;
+        eoff.assign(n + 1, 0);
         std::vector<int32_t> st(n);
         if (tdt_encode_host(codec_.context(), pack_.data(), off.data(), (uint32_t)n, enc_.data(), cap, eoff.data(),
                             st.data()) != TDT_OK)
@@ -290,40 +378,64 @@ public:
         return eoff[n];
     }
 
-    // Receive n frames (each decoding to <= max_msg bytes) and decode them in one GPU call.
-    // out / out_off (n+1) receive the payloads back to back.
-    void receive_batch(size_t n, size_t max_msg, std::vector<uint8_t> &out, std::vector<uint64_t> &out_off) {
-        const size_t fcap = tdt_encode_bound(max_msg, codec_.word_size()) + 64;
+    // The blobs of the last send_batch (frame i = last_batch()[offsets[i] .. offsets[i+1])).
+    const std::vector<uint8_t> &last_batch() const { return enc_; }
+    const std::vector<uint64_t> &last_batch_offsets() const { return eoff_; }
+
+    // Receive n frames (each expected to decode to <= max_msg bytes) and decode them in one GPU
+    // call; out / out_off (n+1) receive the payloads back to back.  Returns the per-message
+    // status: a frame whose header claims more than max_msg is not decoded (TDT_E_CAPACITY,
+    // empty payload) and does not affect the others; decode errors keep their own status.
+    std::vector<int32_t> receive_batch(size_t n, size_t max_msg, std::vector<uint8_t> &out,
+                                       std::vector<uint64_t> &out_off) {
+        const size_t fcap = frame_capacity(max_msg);
         std::vector<uint64_t> boff(n + 1, 0);
-        pack_.resize(n * fcap);
+        std::vector<int32_t> st(n, TDT_OK);
+        std::vector<bool> rejected(n, false);
+        pack_.resize(n * fcap + 4);
         uint64_t decoded = 0;
         for (size_t i = 0; i < n; ++i) {
-            inner_.transport_receive(pack_.data() + boff[i], fcap);
-            boff[i + 1] = boff[i] + inner_.last_received_size();
-            decoded += max_msg;
+            size_t flen = 0;
+            auto pause = std::chrono::microseconds(1);
+            while (!inner_.try_transport_receive(pack_.data() + boff[i], fcap, flen)) {
+                if constexpr (requires(Inner &s) { s.is_connected(); }) {
+                    if (!inner_.is_connected()) throw std::runtime_error("TCP: Not connected");
+                }
+                std::this_thread::sleep_for(pause);
+                if (pause < std::chrono::microseconds(200)) pause *= 2;
+            }
+            const int64_t claimed = tdt_claimed_size(pack_.data() + boff[i], flen);
+            if (claimed > (int64_t)max_msg) {  // replace by an empty UNCP blob
+                static const uint8_t kEmpty[4] = {0x50, 0x43, 0x4E, 0x55};
+                std::memcpy(pack_.data() + boff[i], kEmpty, 4);
+                flen = 4;
+                rejected[i] = true;
+            } else if (claimed > 0) {
+                decoded += (uint64_t)claimed;
+            }
+            boff[i + 1] = boff[i] + flen;
         }
         out.resize(decoded ? decoded : 1);
         out_off.assign(n + 1, 0);
-        std::vector<int32_t> st(n);
-        if (tdt_decode_host(codec_.context(), pack_.data(), boff.data(), (uint32_t)n, out.data(), out.size(),
+        if (tdt_decode_host(codec_.context(), pack_.data(), boff.data(), (uint32_t)n, out.data(), decoded,
                             out_off.data(), st.data()) != TDT_OK)
             throw std::runtime_error(std::string("TDT: GPU batch decode failed: ") + tdt_last_error());
         for (size_t i = 0; i < n; ++i)
-            if (st[i] != TDT_OK) throw std::runtime_error(tdt_status_string(st[i]));
+            if (rejected[i]) st[i] = TDT_E_CAPACITY;
         out.resize(out_off[n]);
+        return st;
     }
 
-    const char *substrate_name() const { return "TDT+PosixTCP"; }
-    bool is_zero_copy() const { return false; }
-    bool is_cross_process() const { return inner_.is_cross_process(); }
-    // wire bytes / payload bytes sent so far
-    double wire_ratio() const { return raw_sent_ ? double(wire_sent_) / double(raw_sent_) : 1.0; }
-
 private:
-    Inner &inner_;
-    HipTDTCompressionProtocol &codec_;
+    // largest frame a <= payload-byte message can arrive as (TDT bound or UNCP n + 4)
+    size_t frame_capacity(size_t payload) const { return tdt_encode_bound(payload, codec_.word_size()) + 64; }
+
+    Inner inner_;
+    HipTDTCompressionProtocol codec_;
+    std::string name_;
     std::vector<uint8_t> stage_, pack_, enc_;
-    size_t raw_sent_ = 0, wire_sent_ = 0;
+    std::vector<uint64_t> eoff_;
+    size_t raw_sent_ = 0, wire_sent_ = 0, last_received_ = 0;
 };
 
 }  // namespace psyne_amd

@@ -81,7 +81,13 @@ typedef struct tdt_ctx tdt_ctx;
 
 void tdt_default_config(tdt_config *cfg);
 
-/* Create a codec context bound to HIP device `device`. */
+/* Create a codec context bound to HIP device `device`.
+ *
+ * Streams: a context owns one device workspace (look-back words, error flags, slot-scan
+ * sums), so its *_batch / *_slots calls must be issued on ONE stream at a time (stream order
+ * keeps consecutive batches apart); use one context per stream for concurrent batches.  The
+ * host calls (tdt_*_host) run on the context's own two pipeline streams and are serialised by
+ * the context; they do not touch the caller's streams. */
 int tdt_ctx_create(int device, const tdt_config *cfg, tdt_ctx **out);
 void tdt_ctx_destroy(tdt_ctx *ctx);
 
@@ -90,8 +96,9 @@ void tdt_ctx_destroy(tdt_ctx *ctx);
 void tdt_ctx_set_metrics(tdt_ctx *ctx, double bandwidth_mbps, double latency_ms, double cpu_usage);
 void tdt_ctx_get_metrics(const tdt_ctx *ctx, double *bandwidth_mbps, double *latency_ms, double *cpu_usage);
 
-/* Hint of the typical message size in bytes: selects the team shape (one 64-lane wave per
- * message for small messages, a 256-lane workgroup otherwise).  Optional. */
+/* Hint of the typical message size in bytes: selects the encode team shape (one 64-lane wave
+ * per message up to 4 KiB, a 512-lane workgroup otherwise).  Optional; any size encodes
+ * correctly with either shape. */
 void tdt_ctx_set_size_hint(tdt_ctx *ctx, uint64_t typical_message_bytes);
 
 /* should_transform (:186-201) for a message of n bytes under the current metrics. */
@@ -159,9 +166,12 @@ int tdt_encode_host(tdt_ctx *ctx, const uint8_t *h_in, const uint64_t *h_in_off,
 int tdt_decode_host(tdt_ctx *ctx, const uint8_t *h_in, const uint64_t *h_in_off, uint32_t n_msgs,
                     uint8_t *h_out, uint64_t out_cap, uint64_t *h_out_off, int32_t *h_status);
 
-/* Device-side invariant flags of the most recent batch on this context (synchronises the
- * device): bit0 look-back timeout, bit1 staging-index guard, bit2 flush-bound guard.  Always
- * 0 for a correct build; the guards turn a logic error into a flag instead of a wild write. */
+/* Device-side invariant flags (synchronises the device): bit0 look-back timeout, bit1
+ * staging-index guard, bit2 flush-bound guard.  Always 0 for a correct build; the guards turn
+ * a logic error into a flag instead of a wild write.  Scope: the most recent compacted
+ * (look-back) batch on the context's workspace, OR-ed with every slotted batch since then
+ * (slotted calls do not clear the word) and with every host-pipeline chunk since the context
+ * was created (sticky). */
 int tdt_ctx_error_flags(tdt_ctx *ctx, uint32_t *flags);
 
 /* Host-memory analyze (analyze_data :206-222): h_entropy n*ws doubles, h_mapping n*ws int32

@@ -102,6 +102,36 @@ int tdt_ref_decode(const uint8_t *blob, size_t len, uint8_t *out, size_t cap,
 
 const char *tdt_ref_last_error(void) { return g_last_error.c_str(); }
 
+// A persistent protocol object (the loopback harness's CPU codec: one per endpoint, as a
+// ProtocolChannel holds one, protocol_demo.cpp:105-216).
+void *tdt_ref_new(float sample_fraction, int word_size, double bandwidth_mbps) {
+    auto *p = new TDTCompressionProtocol(make_cfg(sample_fraction, word_size, 1024));
+    p->update_network_metrics(bandwidth_mbps, 1.0);
+    return p;
+}
+void tdt_ref_free(void *h) { delete static_cast<TDTCompressionProtocol *>(h); }
+// Returns 0, -1 on a reference exception, -2 if cap is too small (out_len = needed).
+int tdt_ref_encode_h(void *h, const uint8_t *data, size_t n, uint8_t *out, size_t cap, size_t *out_len) {
+    std::vector<uint8_t> blob = static_cast<TDTCompressionProtocol *>(h)->encode(const_cast<uint8_t *>(data), n);
+    *out_len = blob.size();
+    if (blob.size() > cap) return -2;
+    std::memcpy(out, blob.data(), blob.size());
+    return 0;
+}
+int tdt_ref_decode_h(void *h, const uint8_t *blob, size_t len, uint8_t *out, size_t cap, size_t *out_len) {
+    try {
+        std::vector<uint8_t> r = static_cast<TDTCompressionProtocol *>(h)->decode(std::vector<uint8_t>(blob, blob + len));
+        *out_len = r.size();
+        if (r.size() > cap) return -2;
+        if (!r.empty()) std::memcpy(out, r.data(), r.size());
+        return 0;
+    } catch (const std::exception &e) {
+        g_last_error = e.what();
+        *out_len = 0;
+        return -1;
+    }
+}
+
 // Timed CPU baseline: `threads` workers, one protocol object each (the reference object
 // is not thread-safe, tdt_compression.hpp:349-360), messages statically interleaved.
 // Each worker encodes then decodes every one of its messages `reps` times and checks

@@ -41,8 +41,10 @@ def build(force: bool = False, verbose: bool = False) -> pathlib.Path:
 
 CPP_TEST_SRC = ROOT / "tests" / "cpp" / "test_protocol.cpp"
 CPP_TEST_BIN = ROOT / "tests" / "cpp" / "test_protocol"
-LOOPBACK_SRC = ROOT / "tools" / "tcp_loopback.cpp"
-LOOPBACK_BIN = ROOT / "tools" / "tcp_loopback"
+LOOPBACK_SRC = ROOT / "tests" / "native" / "tcp_loopback.cpp"
+LOOPBACK_BIN = ROOT / "tests" / "native" / "tcp_loopback"
+SUBSTRATE_TEST_SRC = ROOT / "tests" / "cpp" / "test_substrate.cpp"
+SUBSTRATE_TEST_BIN = ROOT / "tests" / "cpp" / "test_substrate"
 SELFTEST_SRC = ROOT / "tests" / "native" / "selftest.hip"
 SELFTEST_LIB = ROOT / "tests" / "native" / "libtdt_selftest.so"
 
@@ -51,18 +53,27 @@ def build_tests(verbose: bool = False):
     """Test-only native artefacts: the C++ Protocol drop-in test and the primitives self-test."""
     if not CPP_TEST_BIN.exists() or CPP_TEST_BIN.stat().st_mtime < max(
             CPP_TEST_SRC.stat().st_mtime, (ROOT / "include/psyne_amd/hip_tdt_protocol.hpp").stat().st_mtime,
-            LIB.stat().st_mtime):
+            (ROOT / "include/psyne_amd/protocol_stack.hpp").stat().st_mtime, LIB.stat().st_mtime):
         cmd = ["g++", "-std=c++20", "-O2", "-I", str(ROOT / "include"), str(CPP_TEST_SRC), "-o", str(CPP_TEST_BIN),
                "-L", str(PKG), "-lpsyne_tdt", "-Wl,-rpath," + str(PKG), "-Wl,-rpath,$ORIGIN/../../psyne_amd"]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.check_call(cmd)
-    hdrs = [ROOT / "include/psyne_amd/hip_tdt_protocol.hpp", ROOT / "include/psyne_amd/tdt_substrate.hpp"]
+    hdrs = [ROOT / "include/psyne_amd/hip_tdt_protocol.hpp", ROOT / "include/psyne_amd/tdt_substrate.hpp",
+            ROOT / "include/psyne_amd/protocol_stack.hpp"]
     if not LOOPBACK_BIN.exists() or LOOPBACK_BIN.stat().st_mtime < max(
             [LOOPBACK_SRC.stat().st_mtime, LIB.stat().st_mtime] + [h.stat().st_mtime for h in hdrs]):
         cmd = ["g++", "-std=c++20", "-O2", "-I", str(ROOT / "include"), str(LOOPBACK_SRC), "-o", str(LOOPBACK_BIN),
-               "-L", str(PKG), "-lpsyne_tdt", "-pthread", "-Wl,-rpath," + str(PKG),
-               "-Wl,-rpath,$ORIGIN/../psyne_amd"]
+               "-L", str(PKG), "-lpsyne_tdt", "-pthread", "-ldl", "-Wl,-rpath," + str(PKG),
+               "-Wl,-rpath,$ORIGIN/../../psyne_amd"]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.check_call(cmd)
+    if not SUBSTRATE_TEST_BIN.exists() or SUBSTRATE_TEST_BIN.stat().st_mtime < max(
+            [SUBSTRATE_TEST_SRC.stat().st_mtime, LIB.stat().st_mtime] + [h.stat().st_mtime for h in hdrs]):
+        cmd = ["g++", "-std=c++20", "-O2", "-I", str(ROOT / "include"), str(SUBSTRATE_TEST_SRC), "-o",
+               str(SUBSTRATE_TEST_BIN), "-L", str(PKG), "-lpsyne_tdt", "-pthread", "-Wl,-rpath," + str(PKG),
+               "-Wl,-rpath,$ORIGIN/../../psyne_amd"]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.check_call(cmd)

@@ -64,8 +64,11 @@ struct tdt_ctx {
         size_t dev_bytes = 0;
         uint64_t *pin = nullptr;  // pinned: in_off (n+1) | out_off (n+1) | status (n, int32 pairs)
         size_t pin_words = 0;
+        uint32_t *flag = nullptr;  // pinned: the last chunk's device error flags
     } hs[2];
     std::mutex hmu;
+    // error flags of the host pipeline's chunks, OR-ed since the context was created
+    std::atomic<uint32_t> host_flags{0};
 };
 
 namespace {
@@ -144,7 +147,8 @@ int prep(tdt_ctx *c, uint32_t n_msgs, hipStream_t s, uint8_t *&wsp, bool lookbac
             return TDT_OK;
         }
     } else if (!lookback) {
-        return TDT_OK;  // pipeline slot workspaces are zeroed by their own batch calls
+        HIPCHK(hipMemsetAsync(wsp, 0, kCounterBytes, s));  // pipeline chunk: fresh error flags
+        return TDT_OK;
     }
     HIPCHK(hipMemsetAsync(wsp, 0, kCounterBytes + 8ull * n_msgs, s));
     return TDT_OK;
@@ -260,6 +264,8 @@ int ensure_slot(tdt_ctx *c, int k, size_t dev_bytes, size_t pin_words) {
     if (!h.stream) {
         HIPCHK(hipStreamCreateWithFlags(&h.stream, hipStreamNonBlocking));
         HIPCHK(hipEventCreateWithFlags(&h.ev, hipEventDisableTiming));
+        HIPCHK(hipHostMalloc(&h.flag, 4, hipHostMallocDefault));
+        *h.flag = 0;
     }
     if (dev_bytes > h.dev_bytes) {
         if (h.dev) HIPCHK(hipFree(h.dev));
@@ -274,6 +280,16 @@ int ensure_slot(tdt_ctx *c, int k, size_t dev_bytes, size_t pin_words) {
         h.pin_words = 0;
         HIPCHK(hipHostMalloc(&h.pin, 8 * pin_words, hipHostMallocDefault));
         h.pin_words = pin_words;
+    }
+    return TDT_OK;
+}
+
+// After a slot's stream has drained: fold its last chunk's device error flags into the context.
+int sync_slot(tdt_ctx *c, tdt_ctx::HostSlot &h) {
+    HIPCHK(hipStreamSynchronize(h.stream));
+    if (h.flag) {
+        c->host_flags.fetch_or(*h.flag);
+        *h.flag = 0;
     }
     return TDT_OK;
 }
@@ -337,7 +353,8 @@ int host_encode(tdt_ctx *c, const uint8_t *h_in, const uint64_t *h_in_off, uint3
         auto &h = c->hs[ci & 1];
         int st = ensure_slot(c, (int)(ci & 1), chunk_dev_bytes(k), 2ull * (k.n + 1));
         if (st) return st;
-        HIPCHK(hipStreamSynchronize(h.stream));  // the slot's previous chunk is done with its buffers
+        st = sync_slot(c, h);  // the slot's previous chunk is done with its buffers
+        if (st) return st;
         uint64_t *pin_in = h.pin;
         const uint64_t b0 = h_in_off[k.m0];
         for (uint32_t i = 0; i <= k.n; ++i) pin_in[i] = h_in_off[k.m0 + i] - b0;
@@ -350,6 +367,7 @@ int host_encode(tdt_ctx *c, const uint8_t *h_in, const uint64_t *h_in_off, uint3
         st = encode_common(c, psy::MODE_ENCODE, d, doff, k.n, nullptr, d + k.o_out, k.cap, dooff, dst, nullptr, nullptr,
                            nullptr, h.stream, nullptr, nullptr, d + k.o_ws);
         if (st) return st;
+        HIPCHK(hipMemcpyAsync(h.flag, d + k.o_ws + 4, 4, hipMemcpyDeviceToHost, h.stream));
         HIPCHK(hipMemcpyAsync(h.pin + (k.n + 1), dooff, 8ull * (k.n + 1), hipMemcpyDeviceToHost, h.stream));
         if (h_status) HIPCHK(hipMemcpyAsync(h_status + k.m0, dst, 4ull * k.n, hipMemcpyDeviceToHost, h.stream));
         HIPCHK(hipEventRecord(h.ev, h.stream));
@@ -377,7 +395,7 @@ int host_encode(tdt_ctx *c, const uint8_t *h_in, const uint64_t *h_in_off, uint3
     int st = finish(ch.size() - 1);
     if (st) return st;
     for (auto &h : c->hs)
-        if (h.stream) HIPCHK(hipStreamSynchronize(h.stream));
+        if (h.stream && (st = sync_slot(c, h))) return st;
     h_out_off[n_msgs] = base;
     if (capacity) return set_err(TDT_E_CAPACITY, "host output capacity exceeded");
     return TDT_OK;
@@ -407,7 +425,8 @@ int host_decode(tdt_ctx *c, const uint8_t *h_in, const uint64_t *h_in_off, uint3
         auto &h = c->hs[ci & 1];
         int st = ensure_slot(c, (int)(ci & 1), chunk_dev_bytes(k) + 8ull * k.n, 2ull * (k.n + 1));
         if (st) return st;
-        HIPCHK(hipStreamSynchronize(h.stream));
+        st = sync_slot(c, h);
+        if (st) return st;
         uint64_t *pin_in = h.pin, *pin_slot = h.pin + (k.n + 1);
         const uint64_t b0 = h_in_off[k.m0];
         uint64_t acc = 0;
@@ -427,13 +446,16 @@ int host_decode(tdt_ctx *c, const uint8_t *h_in, const uint64_t *h_in_off, uint3
         st = decode_common(c, false, d, doff, k.n, d + k.o_out, 0, nullptr, nullptr, dst, h.stream, dslot, dlen,
                            nullptr, d + k.o_ws);
         if (st) return st;
+        HIPCHK(hipMemcpyAsync(h.flag, d + k.o_ws + 4, 4, hipMemcpyDeviceToHost, h.stream));
         if (acc) HIPCHK(hipMemcpyAsync(h_out + base, d + k.o_out, acc, hipMemcpyDeviceToHost, h.stream));
         HIPCHK(hipMemcpyAsync(lens.data() + k.m0, dlen, 8ull * k.n, hipMemcpyDeviceToHost, h.stream));
         HIPCHK(hipMemcpyAsync(stv.data() + k.m0, dst, 4ull * k.n, hipMemcpyDeviceToHost, h.stream));
         base += acc;
     }
-    for (auto &h : c->hs)
-        if (h.stream) HIPCHK(hipStreamSynchronize(h.stream));
+    for (auto &h : c->hs) {
+        int st = h.stream ? sync_slot(c, h) : TDT_OK;
+        if (st) return st;
+    }
     // offsets; blobs the kernel rejected (status != OK, length 0) leave a gap: compact it
     uint64_t w = 0, r = 0;
     for (uint32_t i = 0; i < n_msgs; ++i) {
@@ -501,6 +523,7 @@ void tdt_ctx_destroy(tdt_ctx *ctx) {
         if (h.stream) (void)hipStreamSynchronize(h.stream);
         if (h.dev) (void)hipFree(h.dev);
         if (h.pin) (void)hipHostFree(h.pin);
+        if (h.flag) (void)hipHostFree(h.flag);
         if (h.ev) (void)hipEventDestroy(h.ev);
         if (h.stream) (void)hipStreamDestroy(h.stream);
     }
@@ -634,11 +657,13 @@ int tdt_decode_host(tdt_ctx *ctx, const uint8_t *h_in, const uint64_t *h_in_off,
 
 int tdt_ctx_error_flags(tdt_ctx *ctx, uint32_t *flags) {
     if (!ctx || !flags) return set_err(TDT_E_ARG, "null argument");
-    *flags = 0;
+    *flags = ctx->host_flags.load();
     if (!ctx->ws) return TDT_OK;
     HIPCHK(hipSetDevice(ctx->device));
     HIPCHK(hipDeviceSynchronize());
-    HIPCHK(hipMemcpy(flags, ctx->ws + 4, 4, hipMemcpyDeviceToHost));
+    uint32_t f = 0;
+    HIPCHK(hipMemcpy(&f, ctx->ws + 4, 4, hipMemcpyDeviceToHost));
+    *flags |= f;
     return TDT_OK;
 }
 

@@ -248,6 +248,12 @@ class TdtCodec:
                                           _ptr(st), self._stream(stream)))
         return hist[:n], ent[:n], mp[:n], st[:n]
 
+    def error_flags(self) -> int:
+        """Device invariant flags (tdt_ctx_error_flags; 0 for a correct build).  Synchronises."""
+        fl = C.c_uint32(0)
+        check(self._lib.tdt_ctx_error_flags(self._h, C.byref(fl)))
+        return int(fl.value)
+
     # ---- host path (socket buffers) -------------------------------------------------------
     def encode_host(self, data: np.ndarray, offsets: np.ndarray):
         data = np.ascontiguousarray(data, dtype=np.uint8)

@@ -2,6 +2,7 @@
 // a Protocol (examples/protocols/protocol_demo.cpp:135-189 in the reference):
 // analyze_data → should_transform → encode → (transport) → decode, through the concept.
 #include <psyne_amd/hip_tdt_protocol.hpp>
+#include <psyne_amd/protocol_stack.hpp>
 
 #include <cstdio>
 #include <random>
@@ -48,6 +49,21 @@ int main() {
     } catch (const std::runtime_error &e) {
         if (std::string(e.what()) != "Invalid TDT magic number") return 1;
     }
-    std::printf("cpp protocol OK ratio=%.4f entropy=%.6f\n", p.transformation_ratio(), p.get_average_entropy());
+    // ProtocolStack (protocol_concepts.hpp:55-69): TDT then identity; decode in reverse order
+    psyne_amd::ProtocolStack stack;
+    stack.push_protocol<psyne_amd::HipTDTCompressionProtocol>(cfg);
+    stack.push_protocol();  // the concept's nullary push: an identity layer
+    stack.update_network_metrics(10.0, 1.0);
+    std::vector<uint8_t> wire = stack.encode_stack(msg.data(), msg.size());
+    if (wire != p.encode(msg.data(), msg.size())) { std::printf("stack encode\n"); return 1; }
+    if (stack.decode_stack(wire) != msg) { std::printf("stack decode\n"); return 1; }
+    if (std::string(stack.stack_name()) != "TDT-Compression -> Identity") { std::printf("stack name\n"); return 1; }
+    auto *tdt = stack.layer<psyne_amd::HipTDTCompressionProtocol>(0);
+    if (!tdt || stack.total_overhead_ms() != tdt->processing_overhead_ms() || !(stack.total_overhead_ms() > 0.0)) {
+        std::printf("stack overhead\n");
+        return 1;
+    }
+    std::printf("cpp protocol OK ratio=%.4f entropy=%.6f stack=%s\n", p.transformation_ratio(), p.get_average_entropy(),
+                stack.stack_name());
     return 0;
 }

@@ -1,0 +1,218 @@
+// tcp_loopback.cpp — loopback TCP harness for the TDT substrate path (BASELINE.json configs[0]).
+// Test/measurement infrastructure (its --codec cpu mode calls the compiled reference).
+//
+// Counterpart of the reference's benchmarks/tcp_tdt_benchmark.cpp (server :297-405, client
+// :407-518): float32 "gradient" tensors of 256 Ki floats (1 MiB; 70 % exact zeros, the rest
+// N(0, 0.01) — tcp_tdt_benchmark.cpp:52-66's GRADIENTS generator) cross a TCP connection on
+// 127.0.0.1 as u32-length frames (tcp_simple.hpp:68-150).  Sender and receiver are two threads
+// of one process, each with its own substrate end; the payloads are generated before the
+// clock starts (the reference times its generator inside the loop, :342-360):
+//
+//   --codec gpu   TdtSubstrate<PosixTcpSubstrate> on both ends (each owns its socket end and a
+//                 GPU codec context): batches of --batch tensors are encoded by one
+//                 tdt_encode_host call and sent as one frame per blob; the receiver takes
+//                 --batch frames and decodes them with one tdt_decode_host call
+//   --codec cpu   the REFERENCE codec (psyne::protocol::TDTCompressionProtocol compiled where
+//                 it lies: oracle/_ref/libtdt_ref.so, loaded at run time), one protocol object
+//                 per endpoint, one message per encode / decode — psyne's own CPU path
+//   --codec none  the same frames without compression (the transport's own ceiling)
+//
+// Every received payload is compared with the original.  --dump DIR writes inputs.bin (the
+// tensors back to back) and frames.bin (u32 length + bytes per sent frame) so that a test can
+// check every wire blob against the oracle.  Effective throughput = original bytes / wall time
+// from the first send to the last verified receive (the reference's "Effective throughput ...
+// MB/s (original)", :401-403).  One JSON line on stdout.
+#include <dlfcn.h>
+
+#include <psyne_amd/tdt_substrate.hpp>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <random>
+#include <string>
+#include <thread>
+#include <vector>
+
+using namespace psyne_amd;
+
+namespace {
+
+// oracle/_ref/libtdt_ref.so (oracle/ref_shim.cpp), resolved next to this binary's repo root
+struct RefCodec {
+    void *lib = nullptr;
+    void *(*make)(float, int, double) = nullptr;
+    void (*release)(void *) = nullptr;
+    int (*enc)(void *, const uint8_t *, size_t, uint8_t *, size_t, size_t *) = nullptr;
+    int (*dec)(void *, const uint8_t *, size_t, uint8_t *, size_t, size_t *) = nullptr;
+    bool load(const std::string &root) {
+        lib = dlopen((root + "/oracle/_ref/libtdt_ref.so").c_str(), RTLD_NOW | RTLD_LOCAL);
+        if (!lib) return false;
+        make = reinterpret_cast<decltype(make)>(dlsym(lib, "tdt_ref_new"));
+        release = reinterpret_cast<decltype(release)>(dlsym(lib, "tdt_ref_free"));
+        enc = reinterpret_cast<decltype(enc)>(dlsym(lib, "tdt_ref_encode_h"));
+        dec = reinterpret_cast<decltype(dec)>(dlsym(lib, "tdt_ref_decode_h"));
+        return make && release && enc && dec;
+    }
+};
+
+std::string repo_root(const char *argv0) {
+    std::string p = argv0;
+    const size_t k = p.rfind("/tests/native/");
+    return k == std::string::npos ? std::string(".") : p.substr(0, k);
+}
+
+}  // namespace
+
+int main(int argc, char **argv) {
+    size_t count = 1000, floats = 256 * 1024, batch = 50;
+    int port = 18080;
+    std::string codec = "gpu", dump;
+    for (int i = 1; i + 1 < argc; i += 2) {
+        const std::string k = argv[i], v = argv[i + 1];
+        if (k == "--count") count = std::stoul(v);
+        else if (k == "--floats") floats = std::stoul(v);
+        else if (k == "--batch") batch = std::stoul(v);
+        else if (k == "--port") port = std::stoi(v);
+        else if (k == "--codec") codec = v;
+        else if (k == "--dump") dump = v;
+    }
+    const size_t bytes = floats * 4;
+    // payloads (GRADIENTS: 70 % zeros, N(0, 0.01) otherwise)
+    std::vector<std::vector<uint8_t>> msgs(count, std::vector<uint8_t>(bytes));
+    {
+        std::mt19937_64 rng(0x5EED0001);
+        std::normal_distribution<float> nd(0.0f, 0.01f);
+        std::uniform_real_distribution<float> u(0.0f, 1.0f);
+        for (auto &m : msgs) {
+            float *f = reinterpret_cast<float *>(m.data());
+            for (size_t i = 0; i < floats; ++i) f[i] = u(rng) < 0.7f ? 0.0f : nd(rng);
+        }
+    }
+    TDTConfig cfg;
+    cfg.sample_fraction = 1.0f;
+    // slow link: compression on (tdt_compression.hpp:192-200) for every codec context
+    TdtSubstrate<PosixTcpSubstrate>::defaults().bandwidth_mbps = 10.0;
+
+    std::unique_ptr<PosixTcpSubstrate> raw_rx, raw_tx;
+    std::unique_ptr<TdtSubstrate<PosixTcpSubstrate>> rx, tx;
+    PosixTcpSubstrate *rx_inner, *tx_inner;
+    if (codec == "gpu") {
+        rx = std::make_unique<TdtSubstrate<PosixTcpSubstrate>>(cfg, "127.0.0.1", (uint16_t)port, true);
+        tx = std::make_unique<TdtSubstrate<PosixTcpSubstrate>>(cfg, "127.0.0.1", (uint16_t)port, false);
+        rx_inner = &rx->inner();
+        tx_inner = &tx->inner();
+    } else {
+        raw_rx = std::make_unique<PosixTcpSubstrate>("127.0.0.1", (uint16_t)port, true);
+        raw_tx = std::make_unique<PosixTcpSubstrate>("127.0.0.1", (uint16_t)port, false);
+        rx_inner = raw_rx.get();
+        tx_inner = raw_tx.get();
+    }
+    if (!rx_inner->wait_for_connection() || !tx_inner->wait_for_connection()) {
+        std::fprintf(stderr, "connection failed\n");
+        return 2;
+    }
+    RefCodec ref;
+    void *ref_tx = nullptr, *ref_rx = nullptr;
+    if (codec == "cpu") {
+        if (!ref.load(repo_root(argv[0]))) {
+            std::fprintf(stderr, "oracle/_ref/libtdt_ref.so not found (make -C oracle in the build container)\n");
+            return 3;
+        }
+        ref_tx = ref.make(1.0f, 4, 10.0);
+        ref_rx = ref.make(1.0f, 4, 10.0);
+    }
+    FILE *frames = nullptr;
+    if (!dump.empty()) {
+        FILE *f = std::fopen((dump + "/inputs.bin").c_str(), "wb");
+        for (auto &m : msgs) std::fwrite(m.data(), 1, m.size(), f);
+        std::fclose(f);
+        frames = std::fopen((dump + "/frames.bin").c_str(), "wb");
+    }
+
+    size_t wire = 0, mismatches = 0;
+    const auto t0 = std::chrono::steady_clock::now();
+    std::thread receiver([&] {
+        std::vector<uint8_t> out;
+        std::vector<uint64_t> off;
+        std::vector<uint8_t> frame(tdt_encode_bound(bytes, 4) + 64), back(bytes);
+        for (size_t b = 0; b < count; b += batch) {
+            const size_t nb = std::min(batch, count - b);
+            if (codec == "gpu") {
+                const std::vector<int32_t> st = rx->receive_batch(nb, bytes, out, off);
+                for (size_t i = 0; i < nb; ++i)
+                    if (st[i] != TDT_OK || off[i + 1] - off[i] != bytes ||
+                        std::memcmp(out.data() + off[i], msgs[b + i].data(), bytes))
+                        ++mismatches;
+                continue;
+            }
+            for (size_t i = 0; i < nb; ++i) {
+                size_t flen = 0;
+                while (!rx_inner->try_transport_receive(frame.data(), frame.size(), flen)) {
+                    if (!rx_inner->is_connected()) {
+                        ++mismatches;
+                        return;
+                    }
+                    std::this_thread::yield();
+                }
+                const uint8_t *got = frame.data();
+                size_t glen = flen;
+                if (codec == "cpu") {
+                    if (ref.dec(ref_rx, frame.data(), flen, back.data(), back.size(), &glen) != 0) glen = 0;
+                    got = back.data();
+                }
+                if (glen != bytes || std::memcmp(got, msgs[b + i].data(), bytes)) ++mismatches;
+            }
+        }
+    });
+    std::vector<const void *> ptrs(batch);
+    std::vector<size_t> sizes(batch, bytes);
+    std::vector<uint8_t> blob(tdt_encode_bound(bytes, 4));
+    for (size_t b = 0; b < count; b += batch) {
+        const size_t nb = std::min(batch, count - b);
+        if (codec == "gpu") {
+            for (size_t i = 0; i < nb; ++i) ptrs[i] = msgs[b + i].data();
+            wire += tx->send_batch(ptrs.data(), sizes.data(), nb);
+            if (frames) {
+                const std::vector<uint8_t> &enc = tx->last_batch();
+                const std::vector<uint64_t> &eo = tx->last_batch_offsets();
+                for (size_t i = 0; i < nb; ++i) {
+                    const uint32_t l = (uint32_t)(eo[i + 1] - eo[i]);
+                    std::fwrite(&l, 4, 1, frames);
+                    std::fwrite(enc.data() + eo[i], 1, l, frames);
+                }
+            }
+            continue;
+        }
+        for (size_t i = 0; i < nb; ++i) {
+            uint8_t *p = msgs[b + i].data();
+            size_t len = bytes;
+            if (codec == "cpu") {
+                if (ref.enc(ref_tx, p, bytes, blob.data(), blob.size(), &len) != 0) return 4;
+                p = blob.data();
+            }
+            tx_inner->transport_send(p, len);
+            if (frames) {
+                const uint32_t l = (uint32_t)len;
+                std::fwrite(&l, 4, 1, frames);
+                std::fwrite(p, 1, len, frames);
+            }
+            wire += len;
+        }
+    }
+    receiver.join();
+    const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (frames) std::fclose(frames);
+    if (ref_tx) ref.release(ref_tx);
+    if (ref_rx) ref.release(ref_rx);
+    const double orig = double(count) * double(bytes);
+    std::printf("{\"harness\": \"tcp_loopback\", \"codec\": \"%s\", \"tensors\": %zu, \"tensor_bytes\": %zu, "
+                "\"batch\": %zu, \"seconds\": %.4f, \"original_MB\": %.1f, \"wire_MB\": %.1f, "
+                "\"compression_ratio\": %.4f, \"effective_MBps\": %.1f, \"network_MBps\": %.1f, "
+                "\"mismatches\": %zu}\n",
+                codec.c_str(), count, bytes, codec == "gpu" ? batch : (size_t)1, secs, orig / 1e6,
+                double(wire) / 1e6, orig / double(wire), orig / 1e6 / secs, double(wire) / 1e6 / secs, mismatches);
+    return mismatches ? 1 : 0;
+}

@@ -121,3 +121,29 @@ def test_large_message(n, lead):
     torch.cuda.synchronize()
     assert int(dst[:3].abs().sum()) == 0
     assert torch.equal(dec[: int(off[-1] - off[0])], d[int(off[0]):])
+
+
+@pytest.mark.timeout(300)
+def test_host_pipeline_multichunk():
+    """tdt_encode_host / tdt_decode_host (pinned staging, two pipeline streams) on a batch of
+    ~600 MB, so it is cut into three 256 MiB chunks that alternate between the two slots: every
+    blob equals the oracle's, the decode restores the input, and no chunk raised a device flag."""
+    rng = np.random.default_rng(77)
+    sizes = np.concatenate([rng.integers(1, 65, 2000) * 64, np.full(9000, 65536, np.int64)])
+    rng.shuffle(sizes)
+    off = np.zeros(sizes.size + 1, np.uint64)
+    off[1:] = np.cumsum(sizes)
+    x = rng.normal(0, 0.01, int(off[-1]) // 4).astype(np.float32)
+    x[rng.random(x.size) < 0.7] = 0
+    buf = x.view(np.uint8)
+    codec = make_codec()
+    enc, eoff, st = codec.encode_host(buf, off)
+    assert int(np.abs(st).sum()) == 0
+    orc = Oracle()
+    idx = np.concatenate([np.arange(50), rng.choice(sizes.size, 400, replace=False), np.arange(sizes.size - 50, sizes.size)])
+    for i in idx:
+        assert enc[eoff[i]:eoff[i + 1]].tobytes() == orc.encode(buf[off[i]:off[i + 1]], bandwidth=10.0), "blob %d" % i
+    dec, doff, dst = codec.decode_host(enc, eoff, int(off[-1]))
+    assert int(np.abs(dst).sum()) == 0
+    assert np.array_equal(doff, off) and np.array_equal(dec, buf)
+    assert codec.error_flags() == 0
