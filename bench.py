@@ -283,11 +283,20 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # PSYNE_BENCH_SHARED_DEVICE=1: rehearsal of the N-rank path on a one-GPU box (every rank on
+    # device 0, gloo for the barrier and reductions); never used for a reported number
+    shared = os.environ.get("PSYNE_BENCH_SHARED_DEVICE") == "1"
+    if shared:
+        local = 0
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if shared:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    red = None if shared else dev  # where the reduction tensors live (gloo: host)
 
     from psyne_amd import TDTConfig, TdtCodec
     from psyne_amd.shard import all_true, reduce_max, reduce_sum
@@ -371,9 +380,9 @@ def main():
     t_enc, t_dec = avg(1, 2), avg(3, 4)
     t_eslot, t_dslot = avg(0, 1), avg(2, 3)
     my_rate = payload * a.steps / elapsed / 2**30
-    job_elapsed = reduce_max(elapsed, dev)  # whole-job time = the slowest rank
-    ok = all_true(ok, dev)
-    job_payload = int(reduce_sum(payload, dev))
+    job_elapsed = reduce_max(elapsed, red)  # whole-job time = the slowest rank
+    ok = all_true(ok, red)
+    job_payload = int(reduce_sum(payload, red))
     ms_per_step = job_elapsed / a.steps * 1e3
     value = job_payload * a.steps / job_elapsed / 2**30
 
@@ -394,7 +403,7 @@ def main():
         tr = load_traffic(key, sha)
         traffic = tr["kernels"][dom].get("hbm_bytes_per_launch") if tr and dom in tr.get("kernels", {}) else None
         cpu = None
-        if a.cpu_seconds > 0 and a.workload == "c3":
+        if a.cpu_seconds > 0 and a.workload == "c3" and world == 1:  # rank 0 at N=1 only
             thr = a.cpu_threads or min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "1024")))
             cpu = cpu_baseline(data, mb, a.cpu_seconds, thr, a.cpu_kind)
         if a.workload == "c3":
@@ -444,6 +453,8 @@ def main():
         }
         if host:
             line["host_inclusive"] = host
+        if shared:
+            line["rehearsal"] = "all ranks on device 0 over gloo (PSYNE_BENCH_SHARED_DEVICE=1): not a scaling number"
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
