@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -69,6 +70,14 @@ struct tdt_ctx {
     std::mutex hmu;
     // error flags of the host pipeline's chunks, OR-ed since the context was created
     std::atomic<uint32_t> host_flags{0};
+    // slotted-encode plan (message classes): counters | small list | medium list (grows with
+    // the batch), and the large-message state: LMeta | tile entries | tile records | bins
+    uint8_t *plan = nullptr;
+    size_t plan_bytes = 0;
+    uint8_t *large = nullptr;
+    uint32_t *plan_host = nullptr;  // pinned: the plan's class counts
+    uint64_t large_min = 256 * 1024;  // messages above this take the tiled path
+    uint32_t tile_cap = ~0u;          // lower tile budget (tests)
 };
 
 namespace {
@@ -98,8 +107,138 @@ bool policy_on(const tdt_ctx *c) {
 
 template <int WS, int TEAM, int G, int MODE, int LB>
 int launch_encode_t(psy::EncodeArgs a, hipStream_t s) {
-    hipLaunchKernelGGL((psy::tdt_encode_kernel<WS, TEAM, G, MODE, LB>), dim3(a.n_msgs), dim3(TEAM), 0, s, a);
+    // one workgroup per message; a launch holds < 2^32 threads, so very large batches take
+    // several (message ids come from the ticket, so the look-back order spans them)
+    const uint32_t maxb = 0xffffffffu / TEAM;
+    for (uint32_t b = 0; b < a.n_msgs; b += maxb)
+        hipLaunchKernelGGL((psy::tdt_encode_kernel<WS, TEAM, G, MODE, LB>), dim3(std::min(maxb, a.n_msgs - b)),
+                           dim3(TEAM), 0, s, a);
     return TDT_OK;
+}
+
+// ---------------------------------------------------------------------------------------
+// Slotted encode (the hot path): a plan kernel sorts the messages into classes — large
+// messages as 64 KiB tiles (histogram + mapping, count, scan, emit), medium messages one
+// 512-lane team each, small ones one wave each — and the host reads its four counts back
+// (16 bytes; the one synchronisation of the call) to size every grid exactly.  Under stream
+// capture (hipGraphs) the counts cannot be read: the grids then cover every message (surplus
+// workgroups exit at once) and large messages stay medium.
+constexpr uint64_t kSmallMax = 4096;  // one-wave teams up to this size
+constexpr uint32_t kLmax = 1u << 16;   // large messages per batch
+// tiles per batch: 64 MiB of span histograms (WS KiB per 512 KiB span) — 8 GiB of large
+// messages at word size 4; further large messages in the batch stay medium
+uint32_t tile_cap_of(int ws) { return (65536u / (uint32_t)ws) * psy::kSpanTiles; }
+size_t large_bytes(int ws) {
+    const size_t tc = tile_cap_of(ws);
+    return (size_t)kLmax * sizeof(psy::LMeta) + tc * (8 + sizeof(psy::TileRec)) + (tc / psy::kSpanTiles) * 8 +
+           (tc / psy::kSpanTiles) * ws * 1024;
+}
+
+int ensure_plan(tdt_ctx *c, uint32_t n) {
+    const size_t need = 256 + 8ull * n;
+    if (need > c->plan_bytes) {
+        if (c->plan) HIPCHK(hipFree(c->plan));
+        c->plan = nullptr;
+        const size_t cap = std::max(need, c->plan_bytes * 2);
+        HIPCHK(hipMalloc(&c->plan, cap));
+        c->plan_bytes = cap;
+    }
+    if (!c->large) {
+        const size_t b = large_bytes(c->cfg.word_size);
+        HIPCHK(hipMalloc(&c->large, b));
+        HIPCHK(hipMemset(c->large, 0, b));
+        HIPCHK(hipHostMalloc(&c->plan_host, 64, hipHostMallocDefault));
+    }
+    return TDT_OK;
+}
+
+// grid of one list-driven launch of TEAM-lane workgroups over `count` entries (launches of
+// < 2^32 threads each)
+template <class F>
+void launch_list(uint32_t count, uint32_t team, F &&launch) {
+    const uint32_t mx = 0xffffffffu / team;
+    for (uint32_t b = 0; b < count; b += mx) launch(b, std::min(mx, count - b));
+}
+
+template <int WS>
+int launch_slotted(tdt_ctx *c, psy::EncodeArgs a, hipStream_t s) {
+    const uint32_t n = a.n_msgs;
+    int st = ensure_plan(c, n);
+    if (st) return st;
+    auto *cnt = reinterpret_cast<uint32_t *>(c->plan);
+    uint32_t *slist = cnt + 64, *mlist = slist + n;
+    const uint32_t tfull = tile_cap_of(WS), scap = tfull / psy::kSpanTiles;
+    const uint32_t lmax = kLmax, tcap = std::min(tfull, std::max(c->tile_cap, psy::kSpanTiles));
+    auto *lmeta = reinterpret_cast<psy::LMeta *>(c->large);
+    auto *tiles = reinterpret_cast<uint64_t *>(c->large + (size_t)lmax * sizeof(psy::LMeta));
+    auto *trec = reinterpret_cast<psy::TileRec *>(reinterpret_cast<uint8_t *>(tiles) + 8ull * tfull);
+    auto *spans = reinterpret_cast<uint64_t *>(reinterpret_cast<uint8_t *>(trec) + sizeof(psy::TileRec) * tfull);
+    auto *shist = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(spans) + 8ull * scap);
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    HIPCHK(hipStreamIsCapturing(s, &cap));
+    const bool capturing = cap != hipStreamCaptureStatusNone;
+    HIPCHK(hipMemsetAsync(cnt, 0, 32, s));
+    psy::PlanArgs p{a.in_off, n, cnt, slist, mlist, tiles, spans, lmeta, lmax, tcap, kSmallMax,
+                    capturing ? ~0ull : c->large_min};
+    const uint32_t per = psy::kPlanThreads * psy::kPlanPer;
+    hipLaunchKernelGGL(psy::tdt_encode_plan_kernel, dim3((uint32_t)(((uint64_t)n + per - 1) / per)),
+                       dim3(psy::kPlanThreads), 0, s, p);
+    HIPCHK(hipGetLastError());
+    uint32_t ns = n, nm = n, nl = 0, nt = 0, nsp = 0;
+    if (!capturing) {
+        HIPCHK(hipMemcpyAsync(c->plan_host, cnt, 32, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        ns = c->plan_host[0];
+        nm = c->plan_host[1];
+        nl = std::min(c->plan_host[2], lmax);
+        nt = std::min(c->plan_host[3], tcap);
+        nsp = std::min(c->plan_host[4], tcap / psy::kSpanTiles);
+    }
+    // large messages: span histograms, mapping, tile counts, scan, emit
+    if (nt) {
+        a.tiles = tiles;
+        a.tile_count = cnt + 3;
+        a.tile_cap = tcap;
+        a.spans = spans;
+        a.lmeta = lmeta;
+        a.trec = trec;
+        a.shist = shist;
+        a.list_base = 0;
+        hipLaunchKernelGGL((psy::tdt_encode_kernel<WS, 512, 8, psy::MODE_ENCODE, 0, 1>), dim3(nsp), dim3(512), 0, s, a);
+        hipLaunchKernelGGL((psy::tdt_encode_kernel<WS, 512, 8, psy::MODE_ENCODE, 0, 4>), dim3(nl), dim3(512), 0, s, a);
+        hipLaunchKernelGGL((psy::tdt_encode_kernel<WS, 512, 8, psy::MODE_ENCODE, 0, 2>), dim3(nt), dim3(512), 0, s, a);
+        hipLaunchKernelGGL((psy::tdt_encode_lscan_kernel<WS>), dim3(nl), dim3(64), 0, s, a, cnt + 2, lmax);
+        hipLaunchKernelGGL((psy::tdt_encode_kernel<WS, 512, 8, psy::MODE_ENCODE, 0, 3>), dim3(nt), dim3(512), 0, s, a);
+    }
+    // medium, then small messages: one workgroup per list entry
+    a.list = mlist;
+    a.list_count = cnt + 1;
+    launch_list(nm, 512, [&](uint32_t b, uint32_t g) {
+        a.list_base = b;
+        hipLaunchKernelGGL((psy::tdt_encode_kernel<WS, 512, 8, psy::MODE_ENCODE, 0, 0>), dim3(g), dim3(512), 0, s, a);
+    });
+    a.list = slist;
+    a.list_count = cnt;
+    launch_list(ns, 64, [&](uint32_t b, uint32_t g) {
+        a.list_base = b;
+        hipLaunchKernelGGL((psy::tdt_encode_kernel<WS, 64, 4, psy::MODE_ENCODE, 0, 0>), dim3(g), dim3(64), 0, s, a);
+    });
+    return TDT_OK;
+}
+
+int launch_slotted_any(tdt_ctx *c, psy::EncodeArgs a, hipStream_t s) {
+    switch (c->cfg.word_size) {
+#ifdef PSY_FAST_BUILD
+        case 4: return launch_slotted<4>(c, a, s);
+#else
+        case 1: return launch_slotted<1>(c, a, s);
+        case 2: return launch_slotted<2>(c, a, s);
+        case 4: return launch_slotted<4>(c, a, s);
+        case 8: return launch_slotted<8>(c, a, s);
+        case 16: return launch_slotted<16>(c, a, s);
+#endif
+    }
+    return set_err(TDT_E_UNSUPPORTED, "word_size not supported on the GPU path");
 }
 
 // messages > 4 KiB: TEAM threads per message, G resident rounds per wave (64 KiB resident)
@@ -189,7 +328,7 @@ int encode_common(tdt_ctx *c, int mode, const uint8_t *d_in, const uint64_t *d_i
     a.slot_off = d_slot_off;
     a.out_len = d_out_len;
     if (mode == psy::MODE_ENCODE) {
-        st = slotted ? launch_encode<psy::MODE_ENCODE, 0>(c, a, s) : launch_encode<psy::MODE_ENCODE, 1>(c, a, s);
+        st = slotted ? launch_slotted_any(c, a, s) : launch_encode<psy::MODE_ENCODE, 1>(c, a, s);
     } else if (mode == psy::MODE_MAPPED) {
         st = launch_encode<psy::MODE_MAPPED, 1>(c, a, s);
     } else {
@@ -509,6 +648,9 @@ int tdt_ctx_create(int device, const tdt_config *cfg, tdt_ctx **out) {
     tdt_ctx *x = new tdt_ctx();
     x->device = device;
     x->cfg = c;
+    // tuning / test overrides: the tiled-path threshold, and a lower tile budget (fallback tests)
+    if (const char *e = std::getenv("PSYNE_TDT_LARGE_MIN")) x->large_min = std::strtoull(e, nullptr, 10);
+    if (const char *e = std::getenv("PSYNE_TDT_TILE_CAP")) x->tile_cap = (uint32_t)std::strtoul(e, nullptr, 10);
     *out = x;
     return TDT_OK;
 }
@@ -518,6 +660,9 @@ void tdt_ctx_destroy(tdt_ctx *ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->ws) (void)hipFree(ctx->ws);
     if (ctx->slot_sums) (void)hipFree(ctx->slot_sums);
+    if (ctx->plan) (void)hipFree(ctx->plan);
+    if (ctx->plan_host) (void)hipHostFree(ctx->plan_host);
+    if (ctx->large) (void)hipFree(ctx->large);
     if (ctx->h_dev) (void)hipFree(ctx->h_dev);
     for (auto &h : ctx->hs) {
         if (h.stream) (void)hipStreamSynchronize(h.stream);

@@ -57,6 +57,32 @@ enum { ST_OK = 0, ST_SHORT = 1, ST_MAGIC = 2, ST_TRUNCATED = 3, ST_BAD_MAPPING =
 constexpr uint32_t kMagicTDT = 0x54445444u;
 constexpr uint32_t kMagicUNCP = 0x554E4350u;
 
+constexpr uint32_t kNone = 0xffffffffu;
+constexpr uint32_t kTileGroups = 4096;  // one tile of a large message: 64 KiB = 512 lanes x 8 rounds
+constexpr uint32_t kSpanTiles = 8;      // the histogram pass takes 8 tiles (512 KiB) per workgroup
+
+// A large message on the tiled path (DESIGN.md §4 "large messages"): written by the plan
+// kernel, completed by the histogram pass (mapping) and the scan (pair count, fit).
+struct LMeta {
+    uint32_t msg;      // message id (kNone: this entry fell back to the whole-message kernel)
+    uint32_t ntiles;   // 64 KiB tiles
+    uint32_t tile0;    // its first tile record
+    uint32_t span0;    // its first span histogram (kSpanTiles tiles per span)
+    uint32_t mapbits;  // bit b = mapping[b] (map pass)
+    uint32_t P0;       // stream 0's pair count (scan)
+    uint32_t fits;     // the blob fits its slot (scan)
+    uint32_t pad;
+};
+// One tile: the count pass writes its local figures, the scan rewrites them in place for the
+// emit pass.  Positions are stream positions (bytes of that stream before them in the message).
+struct TileRec {
+    uint32_t lrs[2];  // count: last run start + 1 in the tile (0: none) | scan: the same before the tile
+    uint32_t frs[2];  // count: first run start in the tile (kNone: none)
+    uint32_t cnt[2];  // count: chunk starts from the first run start on | scan: chunk starts before the tile
+    uint32_t clean;   // count: the tile rules the 255-cap out | scan: and the run carried in has no cap
+    uint32_t pad;
+};
+
 struct EncodeArgs {
     const uint8_t *in;
     const uint64_t *in_off;
@@ -76,6 +102,18 @@ struct EncodeArgs {
     uint64_t *out_len;         // slotted outputs: blob lengths
     uint64_t min_tensor;
     int32_t policy_on;  // bandwidth < threshold && cpu <= threshold (host-evaluated atomics)
+    // persistent slotted kernels: message ids from a class list (null: message id = blockIdx)
+    const uint32_t *list;
+    const uint32_t *list_count;
+    uint32_t list_base;  // first list / tile entry of this launch (grids of < 2^32 threads)
+    // tiled large messages: tile / span entries (L index | tile << 32), their counts (capped)
+    const uint64_t *tiles;
+    const uint32_t *tile_count;
+    uint32_t tile_cap;
+    const uint64_t *spans;
+    LMeta *lmeta;
+    TileRec *trec;
+    uint32_t *shist;  // per span: WS x 256 bin counts
 };
 
 template <int WS, int TEAM>
@@ -135,6 +173,8 @@ __device__ __forceinline__ uint32_t popc(uint32_t x) { return (uint32_t)__builti
 __device__ __forceinline__ uint32_t hibit(uint32_t x) { return 31u - (uint32_t)__builtin_clz(x); }
 __device__ __forceinline__ uint32_t lobit(uint32_t x) { return (uint32_t)__builtin_ctz(x); }
 __device__ __forceinline__ uint32_t umax(uint32_t a, uint32_t b) { return a > b ? a : b; }
+__device__ __forceinline__ uint32_t umin(uint32_t a, uint32_t b) { return a < b ? a : b; }
+__device__ __forceinline__ uint64_t umin64(uint64_t a, uint64_t b) { return a < b ? a : b; }
 __device__ __forceinline__ uint32_t rdlane(uint32_t x, int l) {
     return (uint32_t)__builtin_amdgcn_readlane((int)x, l);
 }
@@ -160,12 +200,17 @@ __device__ __forceinline__ uint32_t spread2(uint32_t e) {
 #endif
 #define PSY_ENC_WAVES(TEAM) ((TEAM) >= 512 ? PSY_ENC_WPE : 1)
 
-template <int WS, int TEAM, int G, int MODE, int LB>
-__global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(EncodeArgs a) {
+// One message — or, TL > 0, part of a large message: TL 1 the histogram of one span of
+// kSpanTiles tiles (UNCP messages: the span's copy), 4 the mapping from the message's span
+// histograms (one team per message), 2 count and 3 emit one 64 KiB tile.
+template <int WS, int TEAM, int G, int MODE, int LB, int TL>
+__device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, uint32_t msg, uint32_t lj,
+                                           uint32_t tile) {
+    static_assert(TL == 0 || (TEAM * G == (int)kTileGroups && MODE == MODE_ENCODE && !LB), "tile shape");
+    constexpr uint32_t kTG = TL == 1 ? kTileGroups * kSpanTiles : kTileGroups;  // groups per team
     using Lay = EncLayout<WS, TEAM>;
     constexpr int W = Lay::W;
     constexpr int WPG = Lay::WPG;
-    __shared__ __attribute__((aligned(16))) uint8_t smem[Lay::BYTES];
     uint32_t *slots = reinterpret_cast<uint32_t *>(smem + Lay::OFF_SLOTS);
     uint32_t *misc = reinterpret_cast<uint32_t *>(smem + Lay::OFF_MISC);
     const int tid = threadIdx.x;
@@ -175,16 +220,6 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     PSY_PROF_BEGIN();
 
-    // Message id: the look-back needs ids in dispatch order (atomic ticket); slotted outputs
-    // have no inter-message dependency, so the workgroup id serves.
-    uint32_t msg;
-    if constexpr (LB) {
-        if (tid == 0) misc[M_MSG] = atomicAdd(a.ticket, 1u);
-        team_sync<W>();
-        msg = __builtin_amdgcn_readfirstlane(misc[M_MSG]);
-    } else {
-        msg = blockIdx.x;
-    }
     if (msg >= a.n_msgs) return;
     PSY_PROF_MARK(0);
 
@@ -238,7 +273,20 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
 
     // ---------------------------------------------------------------- UNCP passthrough
     if (!compress) {
-        if constexpr (MODE != MODE_ANALYZE) {
+        if constexpr (TL == 1) {
+            const uint64_t E = n + 4;
+            const bool fits = E <= slot_e - slot_b;
+            if (tile == 0 && tid == 0) {
+                if (a.status) a.status[msg] = fits ? ST_OK : ST_CAPACITY;
+                if (a.out_len) a.out_len[msg] = fits ? E : 0;
+            }
+            if (fits) {
+                uint8_t *dst = a.out + slot_b;
+                if (tile == 0 && tid < 4) dst[tid] = (uint8_t)(kMagicUNCP >> (8 * tid));
+                const uint64_t t0 = 16ull * kTG * tile;  // this span's bytes
+                team_copy_g2g<TEAM>(dst + 4 + t0, base + t0, n - t0 < 16ull * kTG ? n - t0 : 16ull * kTG);
+            }
+        } else if constexpr (MODE != MODE_ANALYZE && TL == 0) {
             const uint64_t E = n + 4;
             bool fits;
             const uint64_t ob = place(E, fits);
@@ -255,12 +303,15 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
     const uint32_t n32 = (uint32_t)n;
     const uint32_t wc = n32 / WS;
     const uint32_t ngroups = (n32 + 15) / 16;
-    const uint32_t RW = (ngroups + TEAM - 1) / TEAM;  // rounds per wave
+    // the team's groups: the whole message, or one tile of it
+    const uint32_t tg0 = TL ? tile * kTG : 0u;
+    const uint32_t tgn = TL == 4 ? 0u : TL ? umin(ngroups - tg0, kTG) : ngroups;
+    const uint32_t RW = (tgn + TEAM - 1) / TEAM;  // rounds per wave
     const bool al16 = ((uintptr_t)base & 15) == 0;
     // Resident: the rounds fit in VGPRs and every group is a whole aligned 16 bytes, so the
     // loads are straight-line dwordx4s (below); anything else streams.
-    const bool resident = RW <= (uint32_t)G && al16 && (n32 & 15u) == 0;
-    const uint32_t gw0 = (uint32_t)wv * RW * 64;  // first group of this wave
+    const bool resident = TL != 4 && RW <= (uint32_t)G && al16 && (n32 & 15u) == 0;
+    const uint32_t gw0 = tg0 + (uint32_t)wv * RW * 64;  // first group of this wave
 
     auto vbytes = [&](uint32_t g) __attribute__((always_inline)) -> uint32_t {
         const int64_t vb64 = (int64_t)n32 - 16 * (int64_t)g;
@@ -332,10 +383,12 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
     uint32_t *wm = reinterpret_cast<uint32_t *>(smem + Lay::OFF_WMISC);
 
     // ------------------------------------------------------------ mapping (analysis)
-    if constexpr (MODE == MODE_MAPPED) {
+    if constexpr (MODE == MODE_MAPPED || TL == 2 || TL == 3) {
         uint32_t bad = 0;
         if (lane < WS) {
-            const int32_t m = a.mapping_in[(uint64_t)msg * WS + lane];
+            int32_t m;
+            if constexpr (TL == 2 || TL == 3) m = (int32_t)((a.lmeta[lj].mapbits >> lane) & 1u);
+            else m = a.mapping_in[(uint64_t)msg * WS + lane];
             bad = (m < 0 || m > 1) ? 1u : 0u;
             wm[M_MAP + lane] = (uint32_t)(m & 1);
         }
@@ -355,6 +408,18 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
         // lanes to the same address when they hold the same nonzero value.
         uint32_t *hist = reinterpret_cast<uint32_t *>(smem + Lay::OFF_HIST);
         for (int i = tid; i < WS * Lay::PS / 4; i += TEAM) reinterpret_cast<uint4 *>(hist)[i] = make_uint4(0, 0, 0, 0);
+        if constexpr (TL == 4) {
+            // the message's histogram: the sum of its span histograms, into copy 0 of the bins
+            team_sync<W>();
+            const LMeta *lm = a.lmeta + lj;
+            const uint32_t nsp = (lm->ntiles + kSpanTiles - 1) / kSpanTiles;
+            const uint32_t *sh = a.shist + (uint64_t)lm->span0 * WS * 256;
+            for (int i = tid; i < WS * 256; i += TEAM) {
+                uint32_t c = 0;
+                for (uint32_t k = 0; k < nsp; ++k) c += sh[(uint64_t)k * WS * 256 + i];
+                hist[(i >> 8) * Lay::PS + 64 + (i & 255) * Lay::HC] = c;
+            }
+        }
         // glibc log2 tables → LDS (the bins' log2 evaluations read them with per-lane indices)
 #pragma unroll
         for (int k = 0; k < NL2; ++k)
@@ -376,6 +441,7 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
                     atomicAdd(reinterpret_cast<uint32_t *>(smem + Lay::OFF_HIST + (i % WS) * Lay::PS * 4 + ad), 1u);
             }
         };
+        if constexpr (TL != 4)
         for_rounds([&](uint32_t r, uint4 &d, uint32_t &, auto) __attribute__((always_inline)) {
             PSY_ASM_ROUND(H);
             if (full_round(r)) hist_group(d, 16, true);
@@ -383,6 +449,20 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
         });
         team_sync<W>();
         PSY_PROF_MARK(1);
+        if constexpr (TL == 1) {
+            // the span's histogram (its LDS copies and zero bins summed), for the map pass
+            uint32_t *sh = a.shist + ((uint64_t)a.lmeta[lj].span0 + tile) * WS * 256;
+            for (int i = tid; i < WS * 256; i += TEAM) {
+                const int b = i >> 8, v = i & 255;
+                uint32_t c = 0;
+#pragma unroll
+                for (int k = 0; k < Lay::HC; ++k) c += hist[b * Lay::PS + 64 + v * Lay::HC + k];
+                if (v == 0)
+                    for (int z = 0; z < 64; ++z) c += hist[b * Lay::PS + z];
+                sh[i] = c;
+            }
+            return;
+        }
 
         auto count = [&](int b, int v) __attribute__((always_inline)) -> uint32_t {
             uint32_t c = 0;
@@ -599,6 +679,14 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
             if (tid == 0 && a.status) a.status[msg] = ST_OK;
             return;
         }
+        if constexpr (TL == 4) {
+            if (tid == 0) {
+                uint32_t bits = 0;
+                for (int b = 0; b < WS; ++b) bits |= wm[M_MAP + b] << b;
+                a.lmeta[lj].mapbits = bits;
+            }
+            return;
+        }
     }
 
     if constexpr (MODE != MODE_ANALYZE) {
@@ -787,6 +875,11 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
             zk8[c] = Ls[c] == 0u ? 0ull : b8 ? 0x8080808080808080ull : 0x8888888888888888ull;
         }
         uint64_t zacc = 0;
+        // per-lane chunk-start counts.  Streaming teams count run starts in A1 — the chunk
+        // starts when the 255-cap is ruled out, so that A2 (another pass over HBM) is skipped;
+        // resident teams count in A2 (registers only; fewer live values across A1)
+        uint32_t pc0 = 0, pc1 = 0;
+        uint32_t fmx[2] = {0, 0};  // tile count pass: ~(first run start), max-reduced
         {
             uint32_t edc = edc0;
             for_rounds([&](uint32_t r, uint4 &d, uint32_t &cm, auto res) __attribute__((always_inline)) {
@@ -802,12 +895,20 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
                 if constexpr (decltype(res)::value) d = make_uint4(T[0], T[1], T[2], T[3]);
                 const uint32_t m0 = m & lowL0;
                 if (m0) wmax[0] = umax(wmax[0], g * Ls[0] + hibit(m0) + 1u);
+                if constexpr (!decltype(res)::value) pc0 += popc(m0);
+                if constexpr (TL == 2) {
+                    if (m0) fmx[0] = umax(fmx[0], ~(g * Ls[0] + lobit(m0)));
+                }
                 const uint64_t pastm = full_round(r) ? 0ull : (uint64_t)__ballot(g >= ngroups);
                 const uint64_t b0 = (uint64_t)__ballot(m0 != 0u) | pastm;
                 zacc |= (b0 - zk1[0]) & ~b0 & zk8[0];
                 if (ns2) {
                     const uint32_t m1 = m >> L0;
                     if (m1) wmax[1] = umax(wmax[1], g * Ls[1] + hibit(m1) + 1u);
+                    if constexpr (!decltype(res)::value) pc1 += popc(m1);
+                    if constexpr (TL == 2) {
+                        if (m1) fmx[1] = umax(fmx[1], ~(g * Ls[1] + lobit(m1)));
+                    }
                     const uint64_t b1 = (uint64_t)__ballot(m1 != 0u) | pastm;
                     zacc |= (b1 - zk1[1]) & ~b1 & zk8[1];
                 }
@@ -815,14 +916,30 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
         }
         wmax[0] = wave_reduce<OpMax>(wmax[0]);
         wmax[1] = wave_reduce<OpMax>(wmax[1]);
+        if constexpr (TL == 2) {
+            fmx[0] = wave_reduce<OpMax>(fmx[0]);
+            fmx[1] = wave_reduce<OpMax>(fmx[1]);
+        }
         if (lane == 0) {
             slots[wv * 8 + 0] = wmax[0];
             slots[wv * 8 + 1] = wmax[1];
             slots[wv * 8 + 5] = zacc != 0ull ? 1u : 0u;
+            if constexpr (TL == 2) {
+                slots[wv * 8 + 6] = fmx[0];
+                slots[wv * 8 + 7] = fmx[1];
+            }
         }
         team_sync<W>();
         uint32_t rin[2] = {0, 0};  // max (run start + 1) before this wave
         uint32_t capped = 0;       // some wave cannot rule the 255-cap out
+        const TileRec *tr = nullptr;
+        if constexpr (TL == 3) {
+            // the run carried into the tile (scan): as if a wave before wave 0
+            tr = a.trec + a.lmeta[lj].tile0 + tile;
+            rin[0] = tr->lrs[0];
+            rin[1] = tr->lrs[1];
+            capped = tr->clean ? 0u : 1u;
+        }
 #pragma unroll
         for (int ww = 0; ww < W; ++ww) {
             if (ww < wv) {
@@ -837,9 +954,8 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
         PSY_PROF_MARK(3);
 
         // ---------------------------------------------------------- pass A2: chunk starts
-        uint32_t pc0 = 0, pc1 = 0;  // per-lane chunk-start counts
-        uint32_t fb = 0;            // chunk bits of this wave's first group
-        {
+        if (RES || !clean) {
+            pc0 = pc1 = 0;
             uint32_t rcarry[2] = {rin[0], rin[1]};
             uint32_t edc = edc0;
             for_rounds([&](uint32_t r, uint4 &d, uint32_t &cm, auto res) __attribute__((always_inline)) {
@@ -860,7 +976,6 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
                 cm = C;
                 pc0 += popc(C & lowL0);
                 pc1 += popc(C >> L0);
-                if (r == 0) fb = rdlane(C, 0);
             });
         }
         pc0 = wave_reduce<OpAdd>(pc0);
@@ -868,7 +983,6 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
         if (lane == 0) {
             slots[wv * 8 + 2] = pc0;
             slots[wv * 8 + 3] = pc1;
-            slots[wv * 8 + 4] = fb;
         }
         team_sync<W>();
         PSY_PROF_MARK(4);
@@ -883,18 +997,50 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
             ptot[0] += s0;
             ptot[1] += s1;
         }
-        const uint32_t nfb = __builtin_amdgcn_readfirstlane((wv + 1 < W) ? slots[(wv + 1) * 8 + 4] : 0u);
+        if constexpr (TL == 2) {
+            // the tile's local figures for the scan
+            if (tid == 0) {
+                uint32_t l[2] = {0, 0}, f[2] = {0, 0};
+                for (int ww = 0; ww < W; ++ww) {
+                    l[0] = umax(l[0], slots[ww * 8 + 0]);
+                    l[1] = umax(l[1], slots[ww * 8 + 1]);
+                    f[0] = umax(f[0], slots[ww * 8 + 6]);
+                    f[1] = umax(f[1], slots[ww * 8 + 7]);
+                }
+                TileRec *t = a.trec + a.lmeta[lj].tile0 + tile;
+                t->lrs[0] = l[0];
+                t->lrs[1] = l[1];
+                t->frs[0] = ~f[0];
+                t->frs[1] = ~f[1];
+                t->cnt[0] = ptot[0];
+                t->cnt[1] = ptot[1];
+                t->clean = clean ? 1u : 0u;
+            }
+            return;
+        }
         const uint32_t P0 = __builtin_amdgcn_readfirstlane(ptot[0]);
         const uint32_t P1 = ns2 ? __builtin_amdgcn_readfirstlane(ptot[1]) : 0u;
         const uint32_t hdr = 20 + 4 * WS;
-        const uint64_t E = hdr + (4 + 2ull * P0) + (ns2 ? 4 + 2ull * P1 : 0);
-        bool fits;
-        const uint64_t ob = place(E, fits);
-        if (tid == 0 && a.status) a.status[msg] = fits ? ST_OK : ST_CAPACITY;
-        if (!fits) return;
+        uint64_t ob;
+        uint32_t P0m = P0;  // stream 0's pair count in the whole message
+        if constexpr (TL == 3) {
+            const LMeta *lm = a.lmeta + lj;
+            if (!lm->fits) return;  // the scan gave the message CAPACITY
+            ob = slot_b;
+            P0m = lm->P0;
+            pin[0] += tr->cnt[0];  // chunk starts before the tile
+            pin[1] += tr->cnt[1];
+        } else {
+            const uint64_t E = hdr + (4 + 2ull * P0) + (ns2 ? 4 + 2ull * P1 : 0);
+            bool fits;
+            ob = place(E, fits);
+            if (tid == 0 && a.status) a.status[msg] = fits ? ST_OK : ST_CAPACITY;
+            if (!fits) return;
+        }
         // header :84-106 and stream length words :110-112
         uint8_t *dst = a.out + ob;
-        const uint32_t sdata[2] = {hdr + 4, hdr + 4 + 2 * P0 + 4};
+        const uint32_t sdata[2] = {hdr + 4, hdr + 4 + 2 * P0m + 4};
+        if constexpr (TL == 0) {
         for (uint32_t t = tid; t < hdr; t += TEAM) {
             const int f = t >> 2, sh = 8 * (t & 3);
             uint32_t v;
@@ -912,12 +1058,12 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
                 dst[sdata[c] - 4 + (tid & 3)] = (uint8_t)(len >> sh);
             }
         }
+        }
         PSY_PROF_MARK(5);
 
         // ---------------------------------------------------------- pass B: emit pairs
         // Wave-local from here on: per-wave LDS staging, no workgroup barrier.
         const uint32_t wst = Lay::OFF_STAGE + wv * Lay::WSTAGE;
-        uint32_t pr[2] = {(uint32_t)__builtin_amdgcn_readfirstlane(pin[0]), (uint32_t)__builtin_amdgcn_readfirstlane(pin[1])};
         // last chunk start + 1 before this wave: inside the run carried in (start rin - 1),
         // chunks start every 255 bytes (simple_rle_compress :568)
         uint32_t ccarry[2] = {0, 0};
@@ -1216,6 +1362,218 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
     };  // run
     if (resident) run(std::true_type{});
     else run(std::false_type{});
+}
+
+// Message ids: the compacted API's look-back needs them in dispatch order (atomic ticket);
+// slotted batches take them from a class list (or, without one, the workgroup id); TL > 0:
+// one tile of the batch's tile list per workgroup.  (No persistent loops: around this body a
+// loop makes the compiler keep loop-invariant values live across the whole message and
+// spill at the 80-VGPR budget of 6 waves per SIMD.)
+template <int WS, int TEAM, int G, int MODE, int LB, int TL = 0>
+__global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(EncodeArgs a) {
+    using Lay = EncLayout<WS, TEAM>;
+    constexpr int W = Lay::W;
+    __shared__ __attribute__((aligned(16))) uint8_t smem[Lay::BYTES];
+    if constexpr (TL == 4) {
+        const uint32_t lj = blockIdx.x;  // one large message per workgroup
+        const uint32_t msg = a.lmeta[lj].msg;
+        if (msg != kNone) encode_one<WS, TEAM, G, MODE, LB, TL>(a, smem, msg, lj, 0);
+    } else if constexpr (TL > 0) {
+        const uint32_t i = a.list_base + blockIdx.x;  // one span (TL 1) or tile per workgroup
+        const uint64_t e = TL == 1 ? a.spans[i] : a.tiles[i];
+        const uint32_t lj = (uint32_t)e;
+        if (lj == kNone) return;  // a message that did not fit the budgets
+        encode_one<WS, TEAM, G, MODE, LB, TL>(a, smem, a.lmeta[lj].msg, lj, (uint32_t)(e >> 32));
+    } else if constexpr (LB) {
+        uint32_t *misc = reinterpret_cast<uint32_t *>(smem + Lay::OFF_MISC);
+        if (threadIdx.x == 0) misc[M_MSG] = atomicAdd(a.ticket, 1u);
+        team_sync<W>();
+        encode_one<WS, TEAM, G, MODE, LB, 0>(a, smem, __builtin_amdgcn_readfirstlane(misc[M_MSG]), 0, 0);
+    } else {
+        if (!a.list) {
+            encode_one<WS, TEAM, G, MODE, LB, 0>(a, smem, blockIdx.x, 0, 0);
+            return;
+        }
+        // one class-list entry per workgroup (grids sized from the plan's counts; workgroups
+        // past the count, if any, exit at once)
+        const uint32_t i = a.list_base + blockIdx.x;
+        if (i < *a.list_count) encode_one<WS, TEAM, G, MODE, LB, 0>(a, smem, a.list[i], 0, 0);
+    }
+}
+
+// ------------------------------------------------------------------ slotted-batch plan
+// Message classes: small (<= small_max bytes: one-wave teams), medium (512-lane
+// teams), large (> large_min: 64 KiB tiles, so that one message spreads over the whole chip).
+// One thread per message; small / medium ids are appended with one atomic per wave (list order
+// is irrelevant: every blob goes to its own slot).  A large message claims an LMeta entry and a
+// contiguous range of tile entries (tiles of one message in order); when the budgets (lmax
+// entries, tile_cap tiles) are spent it stays medium.
+struct PlanArgs {
+    const uint64_t *in_off;
+    uint32_t n_msgs;
+    uint32_t *cnt;  // [0] small, [1] medium, [2] large entries claimed, [3] tiles, [4] spans claimed
+    uint32_t *slist, *mlist;
+    uint64_t *tiles, *spans;
+    LMeta *lmeta;
+    uint32_t lmax, tile_cap;  // span_cap = tile_cap / kSpanTiles
+    uint64_t small_max, large_min;
+};
+
+constexpr uint32_t kPlanThreads = 1024, kPlanPer = 4;  // messages per plan workgroup: 4096
+
+__global__ __launch_bounds__(kPlanThreads) void tdt_encode_plan_kernel(PlanArgs p) {
+    // one atomic per class and workgroup (a per-wave atomic on one counter serialises ~16 k
+    // times for a million messages): wave ballots → per-wave counts in LDS → workgroup offsets
+    __shared__ uint32_t wcnt[2][kPlanThreads / 64 * kPlanPer];
+    __shared__ uint32_t wbase[2];
+    const int lane = lane_id(), wv = threadIdx.x >> 6;
+    constexpr int NW = kPlanThreads / 64;
+    const uint64_t below = (1ull << lane) - 1ull;
+    int cls[kPlanPer];
+    uint32_t rank[kPlanPer];
+#pragma unroll
+    for (int k = 0; k < (int)kPlanPer; ++k) {
+        const uint32_t i = (blockIdx.x * kPlanPer + k) * kPlanThreads + threadIdx.x;
+        const bool valid = i < p.n_msgs;
+        const uint64_t n = valid ? p.in_off[i + 1] - p.in_off[i] : 0;
+        int c = !valid ? 2 : (n <= p.small_max ? 0 : 1);
+        if (valid && n > p.large_min) {
+            const uint32_t j = atomicAdd(p.cnt + 2, 1u);
+            if (j < p.lmax) {
+                const uint32_t scap = p.tile_cap / kSpanTiles;
+                const uint64_t T = (n + 16ull * kTileGroups - 1) / (16ull * kTileGroups);
+                const uint64_t S = (T + kSpanTiles - 1) / kSpanTiles;
+                const uint32_t Tc = T < (uint64_t)p.tile_cap ? (uint32_t)T : p.tile_cap;
+                const uint32_t Sc = S < (uint64_t)scap ? (uint32_t)S : scap;
+                const uint32_t t0 = atomicAdd(p.cnt + 3, Tc);
+                const uint32_t s0 = atomicAdd(p.cnt + 4, Sc);
+                const bool ok = (uint64_t)t0 + T <= (uint64_t)p.tile_cap && (uint64_t)s0 + S <= (uint64_t)scap;
+                LMeta m{};
+                m.msg = ok ? i : kNone;
+                m.ntiles = (uint32_t)T;
+                m.tile0 = t0;
+                m.span0 = s0;
+                p.lmeta[j] = m;
+                // (entries inside the budget are written even when the message falls back, as kNone)
+                for (uint32_t t = 0; t < Tc && (uint64_t)t0 + t < (uint64_t)p.tile_cap; ++t)
+                    p.tiles[t0 + t] = ok ? ((uint64_t)t << 32 | j) : (uint64_t)kNone;
+                for (uint32_t t = 0; t < Sc && (uint64_t)s0 + t < (uint64_t)scap; ++t)
+                    p.spans[s0 + t] = ok ? ((uint64_t)t << 32 | j) : (uint64_t)kNone;
+                if (ok) c = 2;
+            }
+        }
+        cls[k] = c;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const uint64_t b = __ballot(c == q);
+            rank[k] = c == q ? (uint32_t)__builtin_popcountll(b & below) : rank[k];
+            if (lane == 0) wcnt[q][k * NW + wv] = (uint32_t)__builtin_popcountll(b);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < 2) {  // workgroup totals → one atomic per class
+        uint32_t t = 0;
+        for (int e = 0; e < NW * (int)kPlanPer; ++e) {
+            const uint32_t v = wcnt[threadIdx.x][e];
+            wcnt[threadIdx.x][e] = t;
+            t += v;
+        }
+        wbase[threadIdx.x] = t ? atomicAdd(p.cnt + threadIdx.x, t) : 0u;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < (int)kPlanPer; ++k) {
+        const uint32_t i = (blockIdx.x * kPlanPer + k) * kPlanThreads + threadIdx.x;
+        const int c = cls[k];
+        if (c < 2) (c ? p.mlist : p.slist)[wbase[c] + wcnt[c][k * NW + wv] + rank[k]] = i;
+    }
+}
+
+// Large messages, between the count and emit passes: one wave per message walks its tile
+// records in order — prefix max of the last run start (the run carried into each tile),
+// the 255-cap chunk starts that carried run makes inside the tile before its first own run
+// start, prefix sums of the chunk starts — rewrites the records for the emit pass, and writes
+// the blob's size, status and header.
+template <int WS>
+__global__ __launch_bounds__(64) void tdt_encode_lscan_kernel(EncodeArgs a, const uint32_t *lcnt, uint32_t lmax) {
+    const uint32_t nl = umin(*lcnt, lmax);
+    const int lane = lane_id();
+    for (uint32_t j = blockIdx.x; j < nl; j += gridDim.x) {
+        LMeta *lm = a.lmeta + j;
+        const uint32_t msg = lm->msg;
+        if (msg == kNone) continue;  // fell back to the whole-message kernel
+        const uint64_t n = a.in_off[msg + 1] - a.in_off[msg];
+        const bool compress = a.policy_on && n >= a.min_tensor && (n % 4 == 0) && n >= 64 && (n % WS == 0) &&
+                              n < (1ull << 32);
+        if (!compress) continue;  // UNCP: the histogram pass copied it
+        const uint32_t wc = (uint32_t)n / WS;
+        const uint32_t mapbits = lm->mapbits;
+        const uint32_t k1 = (uint32_t)__builtin_popcount(mapbits & ((1u << WS) - 1u)), k0 = WS - k1;
+        const bool ns2 = k1 != 0;
+        const uint32_t Ls[2] = {(16u / WS) * k0, (16u / WS) * k1};
+        const uint32_t slen[2] = {wc * k0, wc * k1};
+        const uint32_t T = lm->ntiles;
+        TileRec *rec = a.trec + lm->tile0;
+        uint32_t Pt[2] = {0, 0};
+        for (int c = 0; c < (ns2 ? 2 : 1); ++c) {
+            uint32_t carry = 0, P = 0;
+            for (uint32_t t0 = 0; t0 < T; t0 += 64) {
+                const uint32_t t = t0 + (uint32_t)lane;
+                const bool valid = t < T;
+                const uint32_t lrs = valid ? rec[t].lrs[c] : 0u;
+                const uint32_t frs = valid ? rec[t].frs[c] : kNone;
+                const uint32_t cnt = valid ? rec[t].cnt[c] : 0u;
+                const uint32_t incl = wave_incl_scan<OpMax>(lrs);
+                const uint32_t excl = umax(carry, wave_shr1(incl, 0u));
+                const uint64_t ts = (uint64_t)t * kTileGroups * Ls[c];
+                const uint64_t te = umin64((uint64_t)(t + 1) * kTileGroups * Ls[c], slen[c]);
+                const uint64_t e = frs != kNone ? (uint64_t)frs : te;
+                uint32_t h = 0;
+                if (valid && excl > 0 && e > ts) {
+                    const uint64_t rs = excl - 1u;  // < ts: the run carried into the tile
+                    const uint64_t klo = (ts - rs + 254u) / 255u, khi = (e - 1u - rs) / 255u;
+                    h = khi >= klo ? (uint32_t)(khi - klo + 1u) : 0u;
+                }
+                const uint32_t tot = cnt + h;
+                const uint32_t pincl = wave_incl_scan<OpAdd>(tot);
+                if (valid) {
+                    rec[t].lrs[c] = excl;
+                    rec[t].cnt[c] = P + pincl - tot;
+                    if (h) rec[t].clean = 0u;
+                }
+                carry = umax(carry, (uint32_t)__builtin_amdgcn_readlane((int)incl, 63));
+                P += (uint32_t)__builtin_amdgcn_readlane((int)pincl, 63);
+            }
+            Pt[c] = P;
+        }
+        const uint32_t hdr = 20 + 4 * WS;
+        const uint64_t E = hdr + (4 + 2ull * Pt[0]) + (ns2 ? 4 + 2ull * Pt[1] : 0);
+        const uint64_t ob = a.slot_off[msg];
+        const bool fits = E <= a.slot_off[msg + 1] - ob;
+        if (lane == 0) {
+            if (a.status) a.status[msg] = fits ? ST_OK : ST_CAPACITY;
+            if (a.out_len) a.out_len[msg] = fits ? E : 0;
+            lm->P0 = Pt[0];
+            lm->fits = fits ? 1u : 0u;
+        }
+        if (!fits) continue;
+        uint8_t *dst = a.out + ob;
+        for (uint32_t t = (uint32_t)lane; t < hdr; t += 64) {
+            const int f = t >> 2, sh = 8 * (t & 3);
+            uint32_t v;
+            if (f == 0) v = kMagicTDT;
+            else if (f == 1) v = (uint32_t)n;
+            else if (f == 2) v = ns2 ? 2u : 1u;
+            else if (f == 3 || f == 4) v = WS;
+            else v = (mapbits >> (f - 5)) & 1u;
+            dst[t] = (uint8_t)(v >> sh);
+        }
+        if (lane < 8) {
+            const int c = lane >> 2, sh = 8 * (lane & 3);
+            const uint32_t sd0 = hdr + 4, sd1 = hdr + 4 + 2 * Pt[0] + 4;
+            if (c == 0 || ns2) dst[(c ? sd1 : sd0) - 4 + (lane & 3)] = (uint8_t)((2 * Pt[c]) >> sh);
+        }
+    }
 }
 
 }  // namespace psy

@@ -1,0 +1,139 @@
+"""Large messages on the tiled path (DESIGN.md §4 "large messages"): span histograms, the
+mapping pass, per-tile counts, the scan that stitches the run carried across tile boundaries
+(255-cap chunk starts inside the next tile), and the emit pass — every blob compared with the
+oracle byte for byte, then decoded back.  Also the fallback to the whole-message kernel when
+the tile budget is spent."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle.oracle import Oracle
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+
+
+def codec_for(ws=4):
+    from psyne_amd import TDTConfig, TdtCodec
+    c = TdtCodec(TDTConfig(sample_fraction=1.0, word_size=ws))
+    c.set_metrics(10.0, 1.0, 0.5)
+    return c
+
+
+def runs_message(rng, n, mean_run, alphabet=4):
+    """Bytes in runs of geometric length (mean `mean_run`): many runs cross 255 and the tile
+    boundaries, so the cap chunk starts of carried runs land inside later tiles."""
+    out = np.empty(n, np.uint8)
+    i = 0
+    while i < n:
+        L = int(rng.geometric(1.0 / mean_run))
+        out[i:i + L] = rng.integers(0, alphabet)
+        i += L
+    return out
+
+
+def gradient(rng, n):
+    x = rng.normal(0, 0.01, n // 4).astype(np.float32)
+    x[rng.random(x.size) < 0.7] = 0
+    return x.view(np.uint8)
+
+
+def check_batch(msgs, ws=4, lead=0, codec=None):
+    off = np.zeros(len(msgs) + 1, np.int64)
+    off[0] = lead
+    for i, m in enumerate(msgs):
+        off[i + 1] = off[i] + m.size
+    buf = np.zeros(int(off[-1]), np.uint8)
+    for i, m in enumerate(msgs):
+        buf[off[i]:off[i + 1]] = m
+    codec = codec or codec_for(ws)
+    d, o = torch.from_numpy(buf).cuda(), torch.from_numpy(off).cuda()
+    out, slots, lens, st = codec.encode_into(d, o)
+    torch.cuda.synchronize()
+    assert int(st.abs().sum()) == 0
+    orc = Oracle()
+    sl, ln, ob = slots.cpu().numpy(), lens.cpu().numpy(), out.cpu().numpy()
+    for i, m in enumerate(msgs):
+        got = ob[sl[i]:sl[i] + ln[i]].tobytes()
+        want = orc.encode(m, cfg=orc.config(word_size=ws), bandwidth=10.0)
+        assert got == want, "message %d (%d bytes)" % (i, m.size)
+    back, dsl, dln, dst = codec.decode_into(out, slots, in_lengths=lens)
+    torch.cuda.synchronize()
+    assert int(dst.abs().sum()) == 0
+    assert torch.equal(back[: int(off[-1] - off[0])], d[int(off[0]):])
+    assert codec.error_flags() == 0
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("mean_run", [40, 300, 900])
+def test_runs_across_tiles(mean_run):
+    rng = np.random.default_rng(mean_run)
+    check_batch([runs_message(rng, 3 << 20, mean_run), runs_message(rng, (1 << 20) + 4 * 4099, mean_run)])
+
+
+@pytest.mark.timeout(300)
+def test_constant_and_sparse_large():
+    rng = np.random.default_rng(5)
+    zeros = np.zeros(5 << 20, np.uint8)
+    sparse = np.zeros(2 << 20, np.uint8)
+    sparse[rng.integers(0, sparse.size, 200)] = rng.integers(1, 256, 200)
+    # one run starting exactly at a tile boundary and one ending 1 byte past a span boundary
+    edge = np.zeros(1 << 20, np.uint8)
+    edge[65536:65536 + 700] = 7
+    edge[524288 - 5:524288 + 1] = 9
+    check_batch([zeros, sparse, edge])
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("lead", [1, 3, 8])
+def test_mixed_unaligned(lead):
+    """Large messages at misaligned starts (streaming tiles) among small and medium ones."""
+    rng = np.random.default_rng(100 + lead)
+    msgs = []
+    for k in range(24):
+        kind = k % 4
+        if kind == 0:
+            msgs.append(gradient(rng, int(rng.integers(65, 800)) * 4096))
+        elif kind == 1:
+            msgs.append(runs_message(rng, int(rng.integers(70, 700)) * 4096 + 4 * int(rng.integers(0, 1000)), 200))
+        elif kind == 2:
+            msgs.append(rng.integers(0, 256, int(rng.integers(1, 64)) * 64, dtype=np.uint8))
+        else:
+            msgs.append(gradient(rng, int(rng.integers(2, 16)) * 4096))
+    check_batch(msgs, lead=lead)
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("ws", [1, 2, 8, 16])
+def test_word_sizes_large(ws):
+    rng = np.random.default_rng(ws)
+    check_batch([gradient(rng, 3 << 20), runs_message(rng, (2 << 20) + 16 * 1000, 350), gradient(rng, 1 << 19)], ws=ws)
+
+
+@pytest.mark.timeout(300)
+def test_large_uncompressible_passthrough():
+    """Large messages that the policy leaves uncompressed (size not a multiple of 4) are
+    copied span by span."""
+    rng = np.random.default_rng(9)
+    check_batch([rng.integers(0, 256, (3 << 20) + 1, dtype=np.uint8), gradient(rng, 1 << 20),
+                 rng.integers(0, 256, (1 << 20) + 3, dtype=np.uint8)])
+
+
+@pytest.mark.timeout(300)
+def test_tile_budget_fallback():
+    """A tile budget of 64 tiles (4 MiB): the first large messages take the tiled path, the
+    rest the whole-message kernel — the blobs are the same either way."""
+    os.environ["PSYNE_TDT_TILE_CAP"] = "64"
+    try:
+        codec = codec_for(4)
+    finally:
+        del os.environ["PSYNE_TDT_TILE_CAP"]
+    rng = np.random.default_rng(17)
+    msgs = [runs_message(rng, int(rng.integers(5, 20)) * 65536 + 4 * k, 280) for k in range(12)]
+    check_batch(msgs, codec=codec)
