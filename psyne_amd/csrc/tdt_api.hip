@@ -38,6 +38,25 @@ int set_err(int code, const std::string &msg) {
 
 }  // namespace
 
+// Workspace of the slotted calls' plan (message classes / large-message state).  One per
+// stream user: the context's own, and one per host-pipeline slot (those run concurrently).
+struct PlanWS {
+    uint8_t *buf = nullptr;  // counters | lists (grows with the batch)
+    size_t bytes = 0;
+    uint8_t *elarge = nullptr;  // encode: LMeta | tile entries | tile records | span entries | span bins
+    uint8_t *dlarge = nullptr;  // decode: DMeta | block entries | block sums | tile entries | tile blocks
+    uint32_t *host = nullptr;   // pinned: the plan's counts
+    void release() {
+        if (buf) (void)hipFree(buf);
+        if (elarge) (void)hipFree(elarge);
+        if (dlarge) (void)hipFree(dlarge);
+        if (host) (void)hipHostFree(host);
+        buf = elarge = dlarge = nullptr;
+        host = nullptr;
+        bytes = 0;
+    }
+};
+
 struct tdt_ctx {
     int device = 0;
     tdt_config cfg{};
@@ -66,17 +85,13 @@ struct tdt_ctx {
         uint64_t *pin = nullptr;  // pinned: in_off (n+1) | out_off (n+1) | status (n, int32 pairs)
         size_t pin_words = 0;
         uint32_t *flag = nullptr;  // pinned: the last chunk's device error flags
+        PlanWS pw;
     } hs[2];
     std::mutex hmu;
     // error flags of the host pipeline's chunks, OR-ed since the context was created
     std::atomic<uint32_t> host_flags{0};
-    // slotted-encode plan (message classes): counters | small list | medium list (grows with
-    // the batch), and the large-message state: LMeta | tile entries | tile records | bins
-    uint8_t *plan = nullptr;
-    size_t plan_bytes = 0;
-    uint8_t *large = nullptr;
-    uint32_t *plan_host = nullptr;  // pinned: the plan's class counts
-    uint64_t large_min = 256 * 1024;  // messages above this take the tiled path
+    PlanWS pw;                        // the slotted calls' plan workspace
+    uint64_t large_min = 256 * 1024;  // messages (decode: decoded blobs) above this take the tiled path
     uint32_t tile_cap = ~0u;          // lower tile budget (tests)
 };
 
@@ -134,20 +149,24 @@ size_t large_bytes(int ws) {
            (tc / psy::kSpanTiles) * ws * 1024;
 }
 
-int ensure_plan(tdt_ctx *c, uint32_t n) {
+int ensure_plan(PlanWS &w, uint32_t n) {
     const size_t need = 256 + 8ull * n;
-    if (need > c->plan_bytes) {
-        if (c->plan) HIPCHK(hipFree(c->plan));
-        c->plan = nullptr;
-        const size_t cap = std::max(need, c->plan_bytes * 2);
-        HIPCHK(hipMalloc(&c->plan, cap));
-        c->plan_bytes = cap;
+    if (need > w.bytes) {
+        if (w.buf) HIPCHK(hipFree(w.buf));
+        w.buf = nullptr;
+        const size_t cap = std::max(need, w.bytes * 2);
+        HIPCHK(hipMalloc(&w.buf, cap));
+        w.bytes = cap;
     }
-    if (!c->large) {
-        const size_t b = large_bytes(c->cfg.word_size);
-        HIPCHK(hipMalloc(&c->large, b));
-        HIPCHK(hipMemset(c->large, 0, b));
-        HIPCHK(hipHostMalloc(&c->plan_host, 64, hipHostMallocDefault));
+    if (!w.host) HIPCHK(hipHostMalloc(&w.host, 256, hipHostMallocDefault));
+    return TDT_OK;
+}
+
+int ensure_elarge(PlanWS &w, int ws) {
+    if (!w.elarge) {
+        const size_t b = large_bytes(ws);
+        HIPCHK(hipMalloc(&w.elarge, b));
+        HIPCHK(hipMemset(w.elarge, 0, b));
     }
     return TDT_OK;
 }
@@ -161,24 +180,26 @@ void launch_list(uint32_t count, uint32_t team, F &&launch) {
 }
 
 template <int WS>
-int launch_slotted(tdt_ctx *c, psy::EncodeArgs a, hipStream_t s) {
+int launch_slotted(tdt_ctx *c, PlanWS &pw, psy::EncodeArgs a, hipStream_t s) {
     const uint32_t n = a.n_msgs;
-    int st = ensure_plan(c, n);
+    int st = ensure_plan(pw, n);
+    if (!st) st = ensure_elarge(pw, WS);
     if (st) return st;
-    auto *cnt = reinterpret_cast<uint32_t *>(c->plan);
-    uint32_t *slist = cnt + 64, *mlist = slist + n;
+    auto *cnt64 = reinterpret_cast<unsigned long long *>(pw.buf);
+    auto *cnt = reinterpret_cast<uint32_t *>(pw.buf);  // cnt[2k]: the low word of counter k
+    uint32_t *slist = reinterpret_cast<uint32_t *>(pw.buf + 256), *mlist = slist + n;
     const uint32_t tfull = tile_cap_of(WS), scap = tfull / psy::kSpanTiles;
     const uint32_t lmax = kLmax, tcap = std::min(tfull, std::max(c->tile_cap, psy::kSpanTiles));
-    auto *lmeta = reinterpret_cast<psy::LMeta *>(c->large);
-    auto *tiles = reinterpret_cast<uint64_t *>(c->large + (size_t)lmax * sizeof(psy::LMeta));
+    auto *lmeta = reinterpret_cast<psy::LMeta *>(pw.elarge);
+    auto *tiles = reinterpret_cast<uint64_t *>(pw.elarge + (size_t)lmax * sizeof(psy::LMeta));
     auto *trec = reinterpret_cast<psy::TileRec *>(reinterpret_cast<uint8_t *>(tiles) + 8ull * tfull);
     auto *spans = reinterpret_cast<uint64_t *>(reinterpret_cast<uint8_t *>(trec) + sizeof(psy::TileRec) * tfull);
     auto *shist = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(spans) + 8ull * scap);
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     HIPCHK(hipStreamIsCapturing(s, &cap));
     const bool capturing = cap != hipStreamCaptureStatusNone;
-    HIPCHK(hipMemsetAsync(cnt, 0, 32, s));
-    psy::PlanArgs p{a.in_off, n, cnt, slist, mlist, tiles, spans, lmeta, lmax, tcap, kSmallMax,
+    HIPCHK(hipMemsetAsync(cnt, 0, 64, s));
+    psy::PlanArgs p{a.in_off, n, cnt64, slist, mlist, tiles, spans, lmeta, lmax, tcap, kSmallMax,
                     capturing ? ~0ull : c->large_min};
     const uint32_t per = psy::kPlanThreads * psy::kPlanPer;
     hipLaunchKernelGGL(psy::tdt_encode_plan_kernel, dim3((uint32_t)(((uint64_t)n + per - 1) / per)),
@@ -186,18 +207,19 @@ int launch_slotted(tdt_ctx *c, psy::EncodeArgs a, hipStream_t s) {
     HIPCHK(hipGetLastError());
     uint32_t ns = n, nm = n, nl = 0, nt = 0, nsp = 0;
     if (!capturing) {
-        HIPCHK(hipMemcpyAsync(c->plan_host, cnt, 32, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(pw.host, cnt, 64, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
-        ns = c->plan_host[0];
-        nm = c->plan_host[1];
-        nl = std::min(c->plan_host[2], lmax);
-        nt = std::min(c->plan_host[3], tcap);
-        nsp = std::min(c->plan_host[4], tcap / psy::kSpanTiles);
+        const uint64_t *h = reinterpret_cast<const uint64_t *>(pw.host);
+        ns = (uint32_t)h[0];
+        nm = (uint32_t)h[1];
+        nl = (uint32_t)std::min<uint64_t>(h[2], lmax);
+        nt = (uint32_t)std::min<uint64_t>(h[3], tcap);
+        nsp = (uint32_t)std::min<uint64_t>(h[4], tcap / psy::kSpanTiles);
     }
     // large messages: span histograms, mapping, tile counts, scan, emit
     if (nt) {
         a.tiles = tiles;
-        a.tile_count = cnt + 3;
+        a.tile_count = cnt + 6;
         a.tile_cap = tcap;
         a.spans = spans;
         a.lmeta = lmeta;
@@ -207,12 +229,12 @@ int launch_slotted(tdt_ctx *c, psy::EncodeArgs a, hipStream_t s) {
         hipLaunchKernelGGL((psy::tdt_encode_kernel<WS, 512, 8, psy::MODE_ENCODE, 0, 1>), dim3(nsp), dim3(512), 0, s, a);
         hipLaunchKernelGGL((psy::tdt_encode_kernel<WS, 512, 8, psy::MODE_ENCODE, 0, 4>), dim3(nl), dim3(512), 0, s, a);
         hipLaunchKernelGGL((psy::tdt_encode_kernel<WS, 512, 8, psy::MODE_ENCODE, 0, 2>), dim3(nt), dim3(512), 0, s, a);
-        hipLaunchKernelGGL((psy::tdt_encode_lscan_kernel<WS>), dim3(nl), dim3(64), 0, s, a, cnt + 2, lmax);
+        hipLaunchKernelGGL((psy::tdt_encode_lscan_kernel<WS>), dim3(nl), dim3(64), 0, s, a, cnt + 4, lmax);
         hipLaunchKernelGGL((psy::tdt_encode_kernel<WS, 512, 8, psy::MODE_ENCODE, 0, 3>), dim3(nt), dim3(512), 0, s, a);
     }
     // medium, then small messages: one workgroup per list entry
     a.list = mlist;
-    a.list_count = cnt + 1;
+    a.list_count = cnt + 2;
     launch_list(nm, 512, [&](uint32_t b, uint32_t g) {
         a.list_base = b;
         hipLaunchKernelGGL((psy::tdt_encode_kernel<WS, 512, 8, psy::MODE_ENCODE, 0, 0>), dim3(g), dim3(512), 0, s, a);
@@ -226,16 +248,16 @@ int launch_slotted(tdt_ctx *c, psy::EncodeArgs a, hipStream_t s) {
     return TDT_OK;
 }
 
-int launch_slotted_any(tdt_ctx *c, psy::EncodeArgs a, hipStream_t s) {
+int launch_slotted_any(tdt_ctx *c, PlanWS &pw, psy::EncodeArgs a, hipStream_t s) {
     switch (c->cfg.word_size) {
 #ifdef PSY_FAST_BUILD
-        case 4: return launch_slotted<4>(c, a, s);
+        case 4: return launch_slotted<4>(c, pw, a, s);
 #else
-        case 1: return launch_slotted<1>(c, a, s);
-        case 2: return launch_slotted<2>(c, a, s);
-        case 4: return launch_slotted<4>(c, a, s);
-        case 8: return launch_slotted<8>(c, a, s);
-        case 16: return launch_slotted<16>(c, a, s);
+        case 1: return launch_slotted<1>(c, pw, a, s);
+        case 2: return launch_slotted<2>(c, pw, a, s);
+        case 4: return launch_slotted<4>(c, pw, a, s);
+        case 8: return launch_slotted<8>(c, pw, a, s);
+        case 16: return launch_slotted<16>(c, pw, a, s);
 #endif
     }
     return set_err(TDT_E_UNSUPPORTED, "word_size not supported on the GPU path");
@@ -296,7 +318,8 @@ int prep(tdt_ctx *c, uint32_t n_msgs, hipStream_t s, uint8_t *&wsp, bool lookbac
 int encode_common(tdt_ctx *c, int mode, const uint8_t *d_in, const uint64_t *d_in_off, uint32_t n_msgs,
                   const int32_t *d_mapping, uint8_t *d_out, uint64_t out_cap, uint64_t *d_out_off,
                   int32_t *d_status, uint32_t *d_hist, double *d_ent, int32_t *d_map, void *stream,
-                  const uint64_t *d_slot_off = nullptr, uint64_t *d_out_len = nullptr, uint8_t *wsp = nullptr) {
+                  const uint64_t *d_slot_off = nullptr, uint64_t *d_out_len = nullptr, uint8_t *wsp = nullptr,
+                  PlanWS *pws = nullptr) {
     if (!c) return set_err(TDT_E_ARG, "null context");
     if (n_msgs == 0) return TDT_OK;
     if (!d_in_off) return set_err(TDT_E_ARG, "null input offsets");  // d_in may be null: all-empty batch
@@ -328,7 +351,7 @@ int encode_common(tdt_ctx *c, int mode, const uint8_t *d_in, const uint64_t *d_i
     a.slot_off = d_slot_off;
     a.out_len = d_out_len;
     if (mode == psy::MODE_ENCODE) {
-        st = slotted ? launch_slotted_any(c, a, s) : launch_encode<psy::MODE_ENCODE, 1>(c, a, s);
+        st = slotted ? launch_slotted_any(c, pws ? *pws : c->pw, a, s) : launch_encode<psy::MODE_ENCODE, 1>(c, a, s);
     } else if (mode == psy::MODE_MAPPED) {
         st = launch_encode<psy::MODE_MAPPED, 1>(c, a, s);
     } else {
@@ -339,10 +362,67 @@ int encode_common(tdt_ctx *c, int mode, const uint8_t *d_in, const uint64_t *d_i
     return TDT_OK;
 }
 
+// Slotted decode: a plan kernel separates the large blobs (decoded size > large_min) from the
+// rest; the rest decode one wave each; the large ones through the prep / block / scan / tile
+// passes (tdt_decode.h).  Grids are sized from the plan's counts (read back; conservative
+// under stream capture, where every blob takes the one-wave path).
+constexpr uint32_t kDLmax = 1u << 16, kDBcap = 1u << 23, kDTcap = 1u << 20;
+size_t dlarge_bytes() {
+    return (size_t)kDLmax * sizeof(psy::DMeta) + 8ull * kDBcap + 4ull * kDTcap + 8ull * kDTcap;
+}
+
+int launch_decode_slotted(tdt_ctx *c, PlanWS &pw, psy::DecodeArgs a, hipStream_t s) {
+    const uint32_t n = a.n_msgs;
+    int st = ensure_plan(pw, n);
+    if (st) return st;
+    if (!pw.dlarge) HIPCHK(hipMalloc(&pw.dlarge, dlarge_bytes()));
+    auto *cnt = reinterpret_cast<unsigned long long *>(pw.buf);
+    auto *list = reinterpret_cast<uint32_t *>(pw.buf + 256);
+    auto *dmeta = reinterpret_cast<psy::DMeta *>(pw.dlarge);
+    auto *bent = reinterpret_cast<uint32_t *>(pw.dlarge + (size_t)kDLmax * sizeof(psy::DMeta));
+    uint32_t *bsum = bent + kDBcap, *tent = bsum + kDBcap, *tblk = tent + kDTcap;
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    HIPCHK(hipStreamIsCapturing(s, &cap));
+    const bool capturing = cap != hipStreamCaptureStatusNone;
+    HIPCHK(hipMemsetAsync(cnt, 0, 32, s));
+    psy::DPlanArgs p{a.in, a.in_off, a.in_len, n, cnt, list, dmeta, bent, tent, kDLmax, kDBcap, kDTcap,
+                     capturing ? ~0ull : c->large_min};
+    hipLaunchKernelGGL(psy::tdt_decode_plan_kernel, dim3((uint32_t)(((uint64_t)n + 4095) / 4096)), dim3(1024), 0, s, p);
+    HIPCHK(hipGetLastError());
+    uint32_t nn = n, nl = 0, nb = 0, nt = 0;
+    if (!capturing) {
+        HIPCHK(hipMemcpyAsync(pw.host, cnt, 32, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        const uint64_t *h = reinterpret_cast<const uint64_t *>(pw.host);
+        nn = (uint32_t)h[0];
+        nl = (uint32_t)std::min<uint64_t>(h[1], kDLmax);
+        nt = (uint32_t)std::min<uint64_t>(h[2], kDTcap);
+        nb = (uint32_t)std::min<uint64_t>(h[3], kDBcap);
+    }
+    a.list = list;
+    a.dmeta = dmeta;
+    a.bent = bent;
+    a.bsum = bsum;
+    a.tent = tent;
+    a.tblk = tblk;
+    if (nl) {
+        hipLaunchKernelGGL(psy::tdt_decode_lprep_kernel, dim3(nl), dim3(256), 0, s, a);
+        if (nb) hipLaunchKernelGGL(psy::tdt_decode_lblock_kernel, dim3((nb + 3) / 4), dim3(256), 0, s, a, nb);
+        hipLaunchKernelGGL(psy::tdt_decode_lscan_kernel, dim3(nl, 2), dim3(64), 0, s, a);
+        a.list_base = 0;
+        hipLaunchKernelGGL(psy::tdt_decode_ltile_kernel, dim3(nt), dim3(64), 0, s, a);
+    }
+    launch_list(nn, 64, [&](uint32_t b, uint32_t g) {
+        a.list_base = b;
+        hipLaunchKernelGGL((psy::tdt_decode_kernel<0>), dim3(g), dim3(64), 0, s, a);
+    });
+    return TDT_OK;
+}
+
 int decode_common(tdt_ctx *c, bool sizes_only, const uint8_t *d_in, const uint64_t *d_in_off, uint32_t n_msgs,
                   uint8_t *d_out, uint64_t out_cap, uint64_t *d_out_off, uint64_t *d_sizes, int32_t *d_status,
                   void *stream, const uint64_t *d_slot_off = nullptr, uint64_t *d_out_len = nullptr,
-                  const uint64_t *d_in_len = nullptr, uint8_t *wsp = nullptr) {
+                  const uint64_t *d_in_len = nullptr, uint8_t *wsp = nullptr, PlanWS *pws = nullptr) {
     if (!c) return set_err(TDT_E_ARG, "null context");
     if (n_msgs == 0) return TDT_OK;
     if (!d_in_off) return set_err(TDT_E_ARG, "null input offsets");
@@ -369,9 +449,16 @@ int decode_common(tdt_ctx *c, bool sizes_only, const uint8_t *d_in, const uint64
     a.slot_off = d_slot_off;
     a.out_len = d_out_len;
     a.in_len = d_in_len;
-    if (sizes_only) hipLaunchKernelGGL(psy::tdt_decode_sizes_kernel, dim3((n_msgs + 255) / 256), dim3(256), 0, s, a);
-    else if (slotted) hipLaunchKernelGGL((psy::tdt_decode_kernel<0>), dim3(n_msgs), dim3(64), 0, s, a);
-    else hipLaunchKernelGGL((psy::tdt_decode_kernel<1>), dim3(n_msgs), dim3(64), 0, s, a);
+    if (sizes_only) {
+        hipLaunchKernelGGL(psy::tdt_decode_sizes_kernel, dim3((n_msgs + 255) / 256), dim3(256), 0, s, a);
+    } else if (slotted) {
+        st = launch_decode_slotted(c, pws ? *pws : c->pw, a, s);
+        if (st) return st;
+    } else {
+        launch_list(n_msgs, 64, [&](uint32_t, uint32_t g) {  // ids from the ticket
+            hipLaunchKernelGGL((psy::tdt_decode_kernel<1>), dim3(g), dim3(64), 0, s, a);
+        });
+    }
     HIPCHK(hipGetLastError());
     return TDT_OK;
 }
@@ -583,7 +670,7 @@ int host_decode(tdt_ctx *c, const uint8_t *h_in, const uint64_t *h_in_off, uint3
         HIPCHK(hipMemcpyAsync(doff, pin_in, 8ull * (k.n + 1), hipMemcpyHostToDevice, h.stream));
         HIPCHK(hipMemcpyAsync(dslot, pin_slot, 8ull * (k.n + 1), hipMemcpyHostToDevice, h.stream));
         st = decode_common(c, false, d, doff, k.n, d + k.o_out, 0, nullptr, nullptr, dst, h.stream, dslot, dlen,
-                           nullptr, d + k.o_ws);
+                           nullptr, d + k.o_ws, &h.pw);
         if (st) return st;
         HIPCHK(hipMemcpyAsync(h.flag, d + k.o_ws + 4, 4, hipMemcpyDeviceToHost, h.stream));
         if (acc) HIPCHK(hipMemcpyAsync(h_out + base, d + k.o_out, acc, hipMemcpyDeviceToHost, h.stream));
@@ -660,15 +747,14 @@ void tdt_ctx_destroy(tdt_ctx *ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->ws) (void)hipFree(ctx->ws);
     if (ctx->slot_sums) (void)hipFree(ctx->slot_sums);
-    if (ctx->plan) (void)hipFree(ctx->plan);
-    if (ctx->plan_host) (void)hipHostFree(ctx->plan_host);
-    if (ctx->large) (void)hipFree(ctx->large);
+    ctx->pw.release();
     if (ctx->h_dev) (void)hipFree(ctx->h_dev);
     for (auto &h : ctx->hs) {
         if (h.stream) (void)hipStreamSynchronize(h.stream);
         if (h.dev) (void)hipFree(h.dev);
         if (h.pin) (void)hipHostFree(h.pin);
         if (h.flag) (void)hipHostFree(h.flag);
+        h.pw.release();
         if (h.ev) (void)hipEventDestroy(h.ev);
         if (h.stream) (void)hipStreamDestroy(h.stream);
     }

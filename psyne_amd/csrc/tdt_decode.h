@@ -27,6 +27,8 @@
 
 namespace psy {
 
+struct DMeta;
+
 struct DecodeArgs {
     const uint8_t *in;
     const uint64_t *in_off;
@@ -42,9 +44,19 @@ struct DecodeArgs {
     const uint64_t *slot_off;  // slotted outputs (LB = 0)
     uint64_t *out_len;
     const uint64_t *in_len;  // optional blob lengths (blob i = in[in_off[i] .. +in_len[i]))
+    // slotted batches: blob ids from the plan's list (null: blob id = blockIdx)
+    const uint32_t *list;
+    uint32_t list_base;
+    // large blobs (tiled path)
+    DMeta *dmeta;
+    const uint32_t *bent;  // block-slot entries (large-blob index)
+    uint32_t *bsum;        // per 512-pair block: count sum, then (scan) start position
+    const uint32_t *tent;  // tile entries (large-blob index)
+    uint32_t *tblk;        // per tile and referenced stream: the block holding its position - 1
 };
 
 constexpr int kMaxRef = 16;  // referenced streams <= word_size <= 16
+constexpr uint32_t kDecTileGroups = 2048;  // large blobs: 32 KiB of output per tile
 #ifndef PSY_DEC_WR
 #define PSY_DEC_WR 2
 #endif
@@ -194,8 +206,13 @@ struct FastHdr {
     uint64_t osize;
 };
 
+// Groups [g_lo, g_hi) of the output (the whole blob, or one tile of a large one).  A tile that
+// starts inside the blob begins at block b0[r] of stream r — the 512-pair block holding
+// position g_lo·seg_r - 1, whose first pair starts at s0[r] (the scan's prefix); kNone: the
+// stream ends before the tile (s0 = its length).
 __device__ __forceinline__ void decode_fast(const FastHdr &H, uint8_t *smem, const uint8_t *blob, const uint8_t *blim,
-                                            uint8_t *dst, uint32_t ngroups, uint64_t wbytes) {
+                                            uint8_t *dst, uint32_t ngroups, uint64_t wbytes, uint32_t g_lo = 0,
+                                            uint32_t g_hi = 0, const uint32_t *b0 = nullptr, const uint32_t *s0 = nullptr) {
     using Lay = DecLayout;
     constexpr uint32_t WR = kFastWR;
     const uint32_t lane = (uint32_t)lane_id();
@@ -290,9 +307,41 @@ __device__ __forceinline__ void decode_fast(const FastHdr &H, uint8_t *smem, con
         }
     };
 
+    if (g_hi == 0) g_hi = ngroups;
+    if (g_lo > 0) {
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            if (r == 1 && !two) break;
+            const uint32_t P = g_lo * seg[r];
+            const uint32_t b = U(b0[r]), sp = U(s0[r]);
+            if (b == 0xffffffffu) {  // the stream ended before this tile: zeros
+                bidx[r] = np[r];
+                bend[r] = sp;
+                slen[r] = sp;
+                continue;
+            }
+            bidx[r] = 512u * b;
+            bend[r] = sp;
+            load_block(r);
+            // the carry: the value at position P - 1, i.e. of the valid pair with the largest
+            // start <= P - 1 (it lies in this block)
+            uint32_t best = 0, bv = 0;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const uint32_t sti = st[r][i];
+                if (sti != ~0u && sti <= P - 1u && sti + 1u > best) {
+                    best = sti + 1u;
+                    bv = (kp[r][i >> 1] >> (16 * (i & 1))) & 0xffu;
+                }
+            }
+            const uint32_t mx = wave_reduce<OpMax>(best);
+            const uint64_t who = __ballot(best != 0u && best == mx);
+            cv[r] = who ? rdlane(bv, (int)__builtin_ctzll(who)) : 0u;
+        }
+    }
     const bool dal16 = ((uintptr_t)dst & 15) == 0;
     uint32_t win = 0;
-    for (uint32_t gwin = 0; gwin < ngroups; gwin += 64u * WR, ++win) {
+    for (uint32_t gwin = g_lo; gwin < g_hi; gwin += 64u * WR, ++win) {
         const uint32_t gen = win & 7u;
         if (gen == 0) {
             // (re)initialise the head array every 8 windows
@@ -318,7 +367,7 @@ __device__ __forceinline__ void decode_fast(const FastHdr &H, uint8_t *smem, con
         // ---- per round: fill, recombine, store
         for (uint32_t rl = 0; rl < WR; ++rl) {
             const uint32_t g0 = gwin + rl * 64u;
-            if (g0 >= ngroups) break;
+            if (g0 >= g_hi) break;
             const uint32_t hoffb = fh + 2u * rl * 64u * fseg;
             // lanes 8-15 of every 16 read their second half first: with 32-byte lane rows the
             // two ds_read_b128 are then bank-conflict-free (MI355X_MICROARCH.md §LDS groups)
@@ -483,23 +532,14 @@ __device__ __forceinline__ FastHdr parse_fast(const uint8_t *blob, uint64_t len,
     return h;
 }
 
+// One blob, one wave (LB: compacted output by look-back; else its slot).
 template <int LB>
-__global__ __launch_bounds__(64) void tdt_decode_kernel(DecodeArgs a) {
+__device__ __forceinline__ void decode_one(const DecodeArgs &a, uint8_t *smem, uint32_t msg) {
     using Lay = DecLayout;
-    __shared__ __attribute__((aligned(16))) uint8_t smem[Lay::BYTES];
     uint32_t *misc = reinterpret_cast<uint32_t *>(smem + Lay::OFF_MISC);
     uint8_t *hdrc = smem + Lay::OFF_HDR;
     const int lane = lane_id();
     PSY_PROF_BEGIN();
-
-    // look-back needs ids in dispatch order (atomic ticket); slotted outputs do not
-    uint32_t msg = 0;
-    if constexpr (LB) {
-        if (lane == 0) msg = atomicAdd(a.ticket, 1u);
-        msg = __builtin_amdgcn_readfirstlane(msg);
-    } else {
-        msg = blockIdx.x;
-    }
     if (msg >= a.n_msgs) return;
     const uint64_t boff = a.in_off[msg];
     const uint64_t len = a.in_len ? a.in_len[msg] : a.in_off[msg + 1] - boff;
@@ -892,6 +932,277 @@ __global__ __launch_bounds__(64) void tdt_decode_kernel(DecodeArgs a) {
         }
         PSY_PROF_MARK(10);
     }
+}
+
+// ------------------------------------------------------------------ large blobs (slotted)
+// A blob whose decoded size exceeds large_min is decoded by many waves: the
+// prep pass parses its header (wave-parallel) and places it; the block pass sums the counts of
+// every 512-pair block of its referenced streams; the scan turns them into block start
+// positions and records, for every 32 KiB output tile, the block holding the tile's first
+// position - 1 (the carry); the tile pass decodes each tile with the fast path from there.
+// Blobs the fast path does not take are decoded whole, by one wave, in the prep pass.
+struct DMeta {
+    FastHdr H;
+    uint32_t msg, nbs, blk0, ntiles, tile0;
+    uint32_t nb[2];    // 512-pair blocks per referenced stream (prep)
+    uint32_t slen[2];  // decoded stream lengths (scan)
+    uint32_t tiled;    // 1: the tile pass decodes it (kind 1 copy / kind 2 fast path)
+    uint64_t ob;       // output offset (its slot)
+};
+
+struct DPlanArgs {
+    const uint8_t *in;
+    const uint64_t *in_off;
+    const uint64_t *in_len;
+    uint32_t n_msgs;
+    unsigned long long *cnt;  // [0] one-wave blobs, [1] large blobs, [2] tiles, [3] block slots
+    uint32_t *list;
+    DMeta *dmeta;
+    uint32_t *bent, *tent;
+    uint32_t lmax, bcap, tcap;
+    uint64_t large_min;
+};
+
+__global__ __launch_bounds__(1024) void tdt_decode_plan_kernel(DPlanArgs p) {
+    __shared__ uint64_t lds[4 * 16 + 1];
+    // one wave per blob keeps the chip busy while a blob is at most ~1/4096 of the batch's
+    // bytes; only larger blobs (and only above large_min) are worth the tiled passes
+    uint64_t thr = p.large_min;
+    if (p.n_msgs) {
+        const uint64_t last = p.in_len ? p.in_off[p.n_msgs - 1] + p.in_len[p.n_msgs - 1] : p.in_off[p.n_msgs];
+        const uint64_t share = (last - p.in_off[0]) / 4096;
+        thr = share > thr ? share : thr;
+    }
+    uint64_t isl[4], nt[4], nb[4], j[4], t0[4], b0[4], one[4], pos[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t i = (blockIdx.x * 4 + k) * 1024 + threadIdx.x;
+        isl[k] = nt[k] = nb[k] = 0;
+        if (i < p.n_msgs) {
+            const uint64_t boff = p.in_off[i];
+            const uint64_t len = p.in_len ? p.in_len[i] : p.in_off[i + 1] - boff;
+            uint64_t osz = 0, nbs = 0;
+            if (len >= 20) {
+                const uint32_t magic = ld_u32_bytes(p.in + boff);
+                if (magic == kMagicTDT) {
+                    osz = ld_u32_bytes(p.in + boff + 4);
+                    nbs = len / 1024 + 3;  // >= the 512-pair blocks of <= 2 referenced streams
+                } else if (magic == kMagicUNCP) {
+                    osz = len - 4;
+                }
+            }
+            if (osz > thr) {
+                isl[k] = 1;
+                nt[k] = (osz + 16ull * kDecTileGroups - 1) / (16ull * kDecTileGroups);
+                nb[k] = nbs;
+            }
+        }
+    }
+    wg_claim<4>(isl, j, p.cnt + 1, lds);
+    wg_claim<4>(nt, t0, p.cnt + 2, lds);
+    wg_claim<4>(nb, b0, p.cnt + 3, lds);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t i = (blockIdx.x * 4 + k) * 1024 + threadIdx.x;
+        bool large = false;
+        if (isl[k]) {
+            large = j[k] < p.lmax && t0[k] + nt[k] <= p.tcap && b0[k] + nb[k] <= p.bcap;
+            if (large) {
+                DMeta m{};
+                m.msg = i;
+                m.nbs = (uint32_t)nb[k];
+                m.blk0 = (uint32_t)b0[k];
+                m.ntiles = (uint32_t)nt[k];
+                m.tile0 = (uint32_t)t0[k];
+                p.dmeta[j[k]] = m;
+            } else {  // over a budget: the one-wave path; the ranges it claimed stay empty
+                if (j[k] < p.lmax) p.dmeta[j[k]].msg = kNone;
+                for (uint64_t t = t0[k]; t < t0[k] + nt[k] && t < p.tcap; ++t) p.tent[t] = kNone;
+                for (uint64_t b = b0[k]; b < b0[k] + nb[k] && b < p.bcap; ++b) p.bent[b] = kNone;
+            }
+        }
+        one[k] = (i < p.n_msgs && !large) ? 1u : 0u;
+    }
+    wg_claim<4>(one, pos, p.cnt, lds);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (one[k]) p.list[pos[k]] = (blockIdx.x * 4 + k) * 1024 + threadIdx.x;
+}
+
+// Prep: one workgroup per large blob; wave 0 parses and places it, then every thread writes
+// its block-slot and tile entries (kNone where no pass has work).
+__global__ __launch_bounds__(256) void tdt_decode_lprep_kernel(DecodeArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t smem[DecLayout::BYTES];
+    __shared__ uint32_t s_tiled, s_fast;
+    const uint32_t j = blockIdx.x;
+    DMeta *m = a.dmeta + j;
+    const uint32_t msg = m->msg;
+    if (msg == kNone) return;  // over a budget (the plan emptied its ranges)
+    if (threadIdx.x < 64) {
+        const int lane = lane_id();
+        const uint64_t boff = a.in_off[msg];
+        const uint64_t len = a.in_len ? a.in_len[msg] : a.in_off[msg + 1] - boff;
+        const uint8_t *blob = a.in + boff;
+        uint8_t *hdrc = smem + DecLayout::OFF_HDR;
+        {
+            const uint64_t hc = len < (uint64_t)kHdrCache ? len : (uint64_t)kHdrCache;
+            const uint32_t o = (uint32_t)lane * 4u;
+            uint32_t w = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (o + q < hc) w |= (uint32_t)blob[o + q] << (8 * q);
+            reinterpret_cast<uint32_t *>(hdrc)[lane] = w;
+        }
+        team_sync<1>();
+        const uint32_t hcl = len < (uint64_t)kHdrCache ? (uint32_t)len : (uint32_t)kHdrCache;
+        const FastHdr H = parse_fast(blob, len, hdrc, hcl);
+        uint32_t tiled = 0, fast = 0;
+        if (H.kind != 0) {
+            const uint64_t ob = a.slot_off[msg];
+            const bool fits = H.osize <= a.slot_off[msg + 1] - ob;
+            if (lane == 0) {
+                if (a.out_len) a.out_len[msg] = fits ? H.osize : 0;
+                if (a.status) a.status[msg] = fits ? ST_OK : ST_CAPACITY;
+            }
+            if (fits) {
+                tiled = 1;
+                fast = H.kind == 2 ? 1u : 0u;
+                if (H.kind == 2) {
+                    const uint64_t wbytes = (uint64_t)(H.orig / H.ws) * H.ws;
+                    if (H.orig > wbytes) team_zero<64>(a.out + ob + wbytes, H.orig - wbytes);
+                }
+                if (lane == 0) {
+                    m->H = H;
+                    m->ob = ob;
+                    m->nb[0] = (H.np[0] + 511u) / 512u;
+                    m->nb[1] = H.two ? (H.np[1] + 511u) / 512u : 0u;
+                }
+            }
+        } else {
+            decode_one<0>(a, smem, msg);  // any other shape (or an error): one wave, whole
+        }
+        if (lane == 0) {
+            m->tiled = tiled;
+            s_tiled = tiled;
+            s_fast = fast;
+        }
+    }
+    __syncthreads();
+    const uint32_t tv = s_tiled ? j : kNone, bv = s_fast ? j : kNone;
+    for (uint32_t i = threadIdx.x; i < m->ntiles; i += 256) const_cast<uint32_t *>(a.tent)[m->tile0 + i] = tv;
+    for (uint32_t i = threadIdx.x; i < m->nbs; i += 256) const_cast<uint32_t *>(a.bent)[m->blk0 + i] = bv;
+}
+
+// Block pass: one wave per 512-pair block (8 pairs per lane): the block's count sum.
+__global__ __launch_bounds__(256) void tdt_decode_lblock_kernel(DecodeArgs a, uint32_t nslots) {
+    const uint32_t slot = blockIdx.x * 4u + (threadIdx.x >> 6);
+    if (slot >= nslots) return;
+    const uint32_t j = a.bent[slot];
+    if (j == kNone) return;
+    const DMeta *m = a.dmeta + j;
+    const uint32_t idx = slot - m->blk0, nb0 = m->nb[0];
+    const uint32_t r = idx < nb0 ? 0u : 1u;
+    const uint32_t b = r ? idx - nb0 : idx;
+    if (r == 1 && b >= m->nb[1]) return;
+    const uint32_t msg = m->msg;
+    const uint64_t boff = a.in_off[msg];
+    const uint64_t len = a.in_len ? a.in_len[msg] : a.in_off[msg + 1] - boff;
+    const uint8_t *blob = a.in + boff;
+    const uint32_t np = m->H.np[r], soff = m->H.soff[r];
+    const uint32_t p0 = 512u * b + 8u * (uint32_t)lane_id();
+    const uint32_t nv = p0 < np ? (np - p0 < 8u ? np - p0 : 8u) : 0u;
+    const uint4 pv = nv ? ld16_span(blob + soff + 2ull * p0, (int)(2 * nv), blob + len) : make_uint4(0, 0, 0, 0);
+    const uint32_t s2 = (pv.x & 0x00ff00ffu) + (pv.y & 0x00ff00ffu) + (pv.z & 0x00ff00ffu) + (pv.w & 0x00ff00ffu);
+    const uint32_t tot = wave_reduce<OpAdd>((s2 & 0xffffu) + (s2 >> 16));
+    if (lane_id() == 0) a.bsum[m->blk0 + idx] = tot;
+}
+
+// Scan: one wave per large blob and referenced stream: block sums → block start positions
+// (in place), the stream's decoded length, and each tile's carry block.
+__global__ __launch_bounds__(64) void tdt_decode_lscan_kernel(DecodeArgs a) {
+    DMeta *m = a.dmeta + blockIdx.x;
+    const uint32_t r = blockIdx.y;
+    if (m->msg == kNone || !m->tiled || m->H.kind != 2 || (r == 1 && !m->H.two)) return;
+    const uint32_t lane = (uint32_t)lane_id();
+    const uint32_t n = m->nb[r], base = m->blk0 + (r ? m->nb[0] : 0u);
+    const uint64_t TS = (uint64_t)kDecTileGroups * m->H.seg[r];  // stream positions per tile
+    const uint32_t nt = m->ntiles;
+    uint32_t *tb = a.tblk + 2ull * m->tile0 + r;
+    uint64_t run = 0;
+    for (uint32_t c0 = 0; c0 < n; c0 += 64) {
+        const uint32_t b = c0 + lane;
+        const uint32_t v = b < n ? a.bsum[base + b] : 0u;
+        const uint32_t incl = wave_incl_scan<OpAdd>(v);
+        const uint64_t st = run + incl - v;
+        if (b < n) {
+            a.bsum[base + b] = (uint32_t)st;
+            // tiles t >= 1 whose position t·TS - 1 lies in [st, st + v)
+            for (uint64_t t = (st + TS) / TS; t < nt && t * TS <= st + v; ++t) tb[2 * t] = b;
+        }
+        run += rdlane(incl, 63);
+    }
+    if (lane == 0) m->slen[r] = (uint32_t)run;
+}
+
+// Tile pass: one wave per 32 KiB output tile.
+__global__ __launch_bounds__(64) void tdt_decode_ltile_kernel(DecodeArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t smem[DecLayout::BYTES];
+    const uint32_t slot = a.list_base + blockIdx.x;
+    const uint32_t j = a.tent[slot];
+    if (j == kNone) return;
+    const DMeta *m = a.dmeta + j;
+    const uint32_t t = slot - m->tile0;
+    const uint32_t msg = m->msg;
+    const uint64_t boff = a.in_off[msg];
+    const uint64_t len = a.in_len ? a.in_len[msg] : a.in_off[msg + 1] - boff;
+    const uint8_t *blob = a.in + boff;
+    uint8_t *dst = a.out + m->ob;
+    const FastHdr H = m->H;
+    if (H.kind == 1) {
+        const uint64_t o0 = 16ull * kDecTileGroups * t;
+        if (o0 < H.osize) {
+            const uint64_t nb = H.osize - o0 < 16ull * kDecTileGroups ? H.osize - o0 : 16ull * kDecTileGroups;
+            team_copy_g2g<64>(dst + o0, blob + 4 + o0, nb);
+        }
+        return;
+    }
+    const uint64_t wbytes = (uint64_t)(H.orig / H.ws) * H.ws;
+    const uint32_t ngroups = (uint32_t)((wbytes + 15) / 16);
+    const uint32_t g_lo = t * kDecTileGroups;
+    if (g_lo >= ngroups) return;
+    const uint32_t g_hi = ngroups - g_lo < kDecTileGroups ? ngroups : g_lo + kDecTileGroups;
+    uint32_t b0[2] = {0u, 0u}, s0[2] = {0u, 0u};
+    if (g_lo > 0) {
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            if (r == 1 && !H.two) break;
+            const uint32_t P = g_lo * H.seg[r];
+            if (P - 1u >= m->slen[r]) {
+                b0[r] = kNone;
+                s0[r] = m->slen[r];
+            } else {
+                b0[r] = a.tblk[2ull * slot + r];
+                s0[r] = a.bsum[m->blk0 + (r ? m->nb[0] : 0u) + b0[r]];
+            }
+        }
+    }
+    decode_fast(H, smem, blob, blob + len, dst, ngroups, wbytes, g_lo, g_hi, b0, s0);
+}
+
+// Blob ids: the look-back needs them in dispatch order (atomic ticket); slotted batches take
+// them from the plan's list (or, without one, the workgroup id).
+template <int LB>
+__global__ __launch_bounds__(64) void tdt_decode_kernel(DecodeArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t smem[DecLayout::BYTES];
+    uint32_t msg;
+    if constexpr (LB) {
+        uint32_t t = 0;
+        if (lane_id() == 0) t = atomicAdd(a.ticket, 1u);
+        msg = __builtin_amdgcn_readfirstlane(t);
+    } else {
+        msg = a.list ? a.list[a.list_base + blockIdx.x] : a.list_base + blockIdx.x;
+    }
+    decode_one<LB>(a, smem, msg);
 }
 
 }  // namespace psy

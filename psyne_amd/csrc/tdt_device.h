@@ -199,6 +199,42 @@ __device__ __forceinline__ void team_excl_scan(uint32_t (&v)[NV], uint32_t (&tot
     }
 }
 
+// Plan kernels (1024 threads, NK values per thread at slots (k, wave, lane) in message order):
+// the exclusive prefix of v over the workgroup's slots plus ONE atomic add of its total to
+// *ctr — a per-message or per-wave atomic on one counter serialises badly at millions of
+// messages.  lds: NK·16 + 1 words.  All threads must call it.
+template <int NK>
+__device__ __forceinline__ void wg_claim(const uint64_t (&v)[NK], uint64_t (&start)[NK], unsigned long long *ctr,
+                                         uint64_t *lds) {
+    const int lane = (int)__lane_id(), wv = threadIdx.x >> 6;
+    uint64_t incl[NK];
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+        uint64_t x = v[k];
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint64_t y = __shfl_up(x, d);
+            if (lane >= d) x += y;
+        }
+        incl[k] = x;
+        if (lane == 63) lds[k * 16 + wv] = x;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t t = 0;
+        for (int e = 0; e < NK * 16; ++e) {
+            const uint64_t x = lds[e];
+            lds[e] = t;
+            t += x;
+        }
+        lds[NK * 16] = t ? atomicAdd(ctr, (unsigned long long)t) : 0ull;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < NK; ++k) start[k] = lds[NK * 16] + lds[k * 16 + wv] + incl[k] - v[k];
+    __syncthreads();  // lds is reused by the next call
+}
+
 template <int W>
 __device__ __forceinline__ void team_sync() {
     if constexpr (W == 1) {

@@ -1411,7 +1411,7 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
 struct PlanArgs {
     const uint64_t *in_off;
     uint32_t n_msgs;
-    uint32_t *cnt;  // [0] small, [1] medium, [2] large entries claimed, [3] tiles, [4] spans claimed
+    unsigned long long *cnt;  // [0] small, [1] medium, [2] large entries, [3] tiles, [4] spans claimed
     uint32_t *slist, *mlist;
     uint64_t *tiles, *spans;
     LMeta *lmeta;
@@ -1419,73 +1419,57 @@ struct PlanArgs {
     uint64_t small_max, large_min;
 };
 
-constexpr uint32_t kPlanThreads = 1024, kPlanPer = 4;  // messages per plan workgroup: 4096
+constexpr uint32_t kPlanThreads = 1024, kPlanPer = 2;  // messages per plan workgroup: 2048
 
 __global__ __launch_bounds__(kPlanThreads) void tdt_encode_plan_kernel(PlanArgs p) {
-    // one atomic per class and workgroup (a per-wave atomic on one counter serialises ~16 k
-    // times for a million messages): wave ballots → per-wave counts in LDS → workgroup offsets
-    __shared__ uint32_t wcnt[2][kPlanThreads / 64 * kPlanPer];
-    __shared__ uint32_t wbase[2];
-    const int lane = lane_id(), wv = threadIdx.x >> 6;
-    constexpr int NW = kPlanThreads / 64;
-    const uint64_t below = (1ull << lane) - 1ull;
-    int cls[kPlanPer];
-    uint32_t rank[kPlanPer];
+    __shared__ uint64_t lds[kPlanPer * 16 + 1];
+    const uint32_t scap = p.tile_cap / kSpanTiles;
+    uint64_t n[kPlanPer], isl[kPlanPer], T[kPlanPer], S[kPlanPer], j[kPlanPer], t0[kPlanPer], s0[kPlanPer];
 #pragma unroll
     for (int k = 0; k < (int)kPlanPer; ++k) {
         const uint32_t i = (blockIdx.x * kPlanPer + k) * kPlanThreads + threadIdx.x;
-        const bool valid = i < p.n_msgs;
-        const uint64_t n = valid ? p.in_off[i + 1] - p.in_off[i] : 0;
-        int c = !valid ? 2 : (n <= p.small_max ? 0 : 1);
-        if (valid && n > p.large_min) {
-            const uint32_t j = atomicAdd(p.cnt + 2, 1u);
-            if (j < p.lmax) {
-                const uint32_t scap = p.tile_cap / kSpanTiles;
-                const uint64_t T = (n + 16ull * kTileGroups - 1) / (16ull * kTileGroups);
-                const uint64_t S = (T + kSpanTiles - 1) / kSpanTiles;
-                const uint32_t Tc = T < (uint64_t)p.tile_cap ? (uint32_t)T : p.tile_cap;
-                const uint32_t Sc = S < (uint64_t)scap ? (uint32_t)S : scap;
-                const uint32_t t0 = atomicAdd(p.cnt + 3, Tc);
-                const uint32_t s0 = atomicAdd(p.cnt + 4, Sc);
-                const bool ok = (uint64_t)t0 + T <= (uint64_t)p.tile_cap && (uint64_t)s0 + S <= (uint64_t)scap;
+        n[k] = i < p.n_msgs ? p.in_off[i + 1] - p.in_off[i] : 0;
+        isl[k] = i < p.n_msgs && n[k] > p.large_min ? 1u : 0u;
+        T[k] = isl[k] ? (n[k] + 16ull * kTileGroups - 1) / (16ull * kTileGroups) : 0;
+        S[k] = (T[k] + kSpanTiles - 1) / kSpanTiles;
+    }
+    wg_claim<kPlanPer>(isl, j, p.cnt + 2, lds);
+    wg_claim<kPlanPer>(T, t0, p.cnt + 3, lds);
+    wg_claim<kPlanPer>(S, s0, p.cnt + 4, lds);
+    uint64_t sm[kPlanPer], md[kPlanPer], ps[kPlanPer], pm[kPlanPer];
+#pragma unroll
+    for (int k = 0; k < (int)kPlanPer; ++k) {
+        const uint32_t i = (blockIdx.x * kPlanPer + k) * kPlanThreads + threadIdx.x;
+        bool large = false;
+        if (isl[k]) {
+            large = j[k] < p.lmax && t0[k] + T[k] <= p.tile_cap && s0[k] + S[k] <= scap;
+            if (large) {
                 LMeta m{};
-                m.msg = ok ? i : kNone;
-                m.ntiles = (uint32_t)T;
-                m.tile0 = t0;
-                m.span0 = s0;
-                p.lmeta[j] = m;
-                // (entries inside the budget are written even when the message falls back, as kNone)
-                for (uint32_t t = 0; t < Tc && (uint64_t)t0 + t < (uint64_t)p.tile_cap; ++t)
-                    p.tiles[t0 + t] = ok ? ((uint64_t)t << 32 | j) : (uint64_t)kNone;
-                for (uint32_t t = 0; t < Sc && (uint64_t)s0 + t < (uint64_t)scap; ++t)
-                    p.spans[s0 + t] = ok ? ((uint64_t)t << 32 | j) : (uint64_t)kNone;
-                if (ok) c = 2;
+                m.msg = i;
+                m.ntiles = (uint32_t)T[k];
+                m.tile0 = (uint32_t)t0[k];
+                m.span0 = (uint32_t)s0[k];
+                p.lmeta[j[k]] = m;
+            } else if (j[k] < p.lmax) {
+                p.lmeta[j[k]].msg = kNone;
             }
+            // tile / span entries (kNone: the message is over a budget and stays medium)
+            for (uint64_t t = 0; t < T[k] && t0[k] + t < p.tile_cap; ++t)
+                p.tiles[t0[k] + t] = large ? (t << 32 | j[k]) : (uint64_t)kNone;
+            for (uint64_t t = 0; t < S[k] && s0[k] + t < scap; ++t)
+                p.spans[s0[k] + t] = large ? (t << 32 | j[k]) : (uint64_t)kNone;
         }
-        cls[k] = c;
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const uint64_t b = __ballot(c == q);
-            rank[k] = c == q ? (uint32_t)__builtin_popcountll(b & below) : rank[k];
-            if (lane == 0) wcnt[q][k * NW + wv] = (uint32_t)__builtin_popcountll(b);
-        }
+        const bool valid = i < p.n_msgs;
+        sm[k] = valid && !large && n[k] <= p.small_max ? 1u : 0u;
+        md[k] = valid && !large && n[k] > p.small_max ? 1u : 0u;
     }
-    __syncthreads();
-    if (threadIdx.x < 2) {  // workgroup totals → one atomic per class
-        uint32_t t = 0;
-        for (int e = 0; e < NW * (int)kPlanPer; ++e) {
-            const uint32_t v = wcnt[threadIdx.x][e];
-            wcnt[threadIdx.x][e] = t;
-            t += v;
-        }
-        wbase[threadIdx.x] = t ? atomicAdd(p.cnt + threadIdx.x, t) : 0u;
-    }
-    __syncthreads();
+    wg_claim<kPlanPer>(sm, ps, p.cnt + 0, lds);
+    wg_claim<kPlanPer>(md, pm, p.cnt + 1, lds);
 #pragma unroll
     for (int k = 0; k < (int)kPlanPer; ++k) {
         const uint32_t i = (blockIdx.x * kPlanPer + k) * kPlanThreads + threadIdx.x;
-        const int c = cls[k];
-        if (c < 2) (c ? p.mlist : p.slist)[wbase[c] + wcnt[c][k * NW + wv] + rank[k]] = i;
+        if (sm[k]) p.slist[ps[k]] = i;
+        if (md[k]) p.mlist[pm[k]] = i;
     }
 }
 

@@ -137,3 +137,76 @@ def test_tile_budget_fallback():
     rng = np.random.default_rng(17)
     msgs = [runs_message(rng, int(rng.integers(5, 20)) * 65536 + 4 * k, 280) for k in range(12)]
     check_batch(msgs, codec=codec)
+
+
+def parse_blob(b):
+    """(header words, mapping, [stream bytes]) of a TDT blob."""
+    w = np.frombuffer(b[:20], np.uint32)
+    msize = int(w[4])
+    mapping = np.frombuffer(b[20:20 + 4 * msize], np.int32).copy()
+    off, streams = 20 + 4 * msize, []
+    for _ in range(int(w[2])):
+        ln = int.from_bytes(b[off:off + 4], "little")
+        streams.append(b[off + 4:off + 4 + ln])
+        off += 4 + ln
+    return w.copy(), mapping, streams
+
+
+def build_blob(w, mapping, streams):
+    out = w.astype(np.uint32).tobytes() + mapping.astype(np.int32).tobytes()
+    for st in streams:
+        out += len(st).to_bytes(4, "little") + st
+    return out
+
+
+def decode_vs_oracle(blobs):
+    from psyne_amd import TDTConfig, TdtCodec
+    codec = TdtCodec(TDTConfig(sample_fraction=1.0))
+    off = np.zeros(len(blobs) + 1, np.int64)
+    off[1:] = np.cumsum([len(b) for b in blobs])
+    buf = np.frombuffer(b"".join(blobs), np.uint8).copy()
+    d, o = torch.from_numpy(buf).cuda(), torch.from_numpy(off).cuda()
+    out, slots, lens, st = codec.decode_into(d, o)
+    torch.cuda.synchronize()
+    orc = Oracle()
+    sl, ln, ob, sts = slots.cpu().numpy(), lens.cpu().numpy(), out.cpu().numpy(), st.cpu().numpy()
+    for i, b in enumerate(blobs):
+        ost, want = orc.decode(b)
+        assert int(sts[i]) == ost, "blob %d status %d vs oracle %d" % (i, sts[i], ost)
+        if ost == 0:
+            assert ob[sl[i]:sl[i] + ln[i]].tobytes() == want, "blob %d bytes" % i
+    assert codec.error_flags() == 0
+
+
+@pytest.mark.timeout(300)
+def test_large_decode_crafted():
+    rng = np.random.default_rng(23)
+    orc = Oracle()
+    good = orc.encode(gradient(rng, 3 << 20), bandwidth=10.0)
+    w, mp, streams = parse_blob(good)
+    assert len(streams) == 2
+    # stream 1 cut to a third of its pairs: its positions past that decode as zeros
+    s1 = streams[1][: (len(streams[1]) // 6) * 2]
+    short = build_blob(w, mp, [streams[0], s1])
+    # stream 0 empty, stream 1 whole
+    empty0 = build_blob(w, mp, [b"", streams[1]])
+    # truncated blob (stream table runs past the end)
+    trunc = good[:-7]
+    # a stream with count-0 pairs sprinkled in (emit nothing)
+    s0 = bytearray(streams[0])
+    for k in range(0, len(s0) - 1, 2 * 997):
+        s0[k] = 0
+    zeros = build_blob(w, mp, [bytes(s0), streams[1]])
+    decode_vs_oracle([good, short, empty0, trunc, zeros])
+
+
+@pytest.mark.timeout(300)
+def test_large_decode_generic_shapes():
+    """A large blob the fast path does not take (word size 8, three positions in stream 1:
+    6-byte segments): decoded whole by one wave in the prep pass, still bit-exact."""
+    rng = np.random.default_rng(29)
+    orc = Oracle()
+    x = gradient(rng, 2 << 20)
+    b8 = orc.encode(x, cfg=orc.config(word_size=8), bandwidth=10.0, mapping=[1, 1, 1, 0, 0, 0, 0, 0])
+    assert parse_blob(b8)[0][3] == 8
+    decode_vs_oracle([b8, orc.encode(x, bandwidth=10.0)])
