@@ -17,9 +17,12 @@ LIB = PKG / "libpsyne_tdt.so"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("PSYNE_ARCH", "gfx950")
 
-SOURCES = [CSRC / "tdt_api.hip"]
-# every header under csrc/ (tdt_api.hip includes them all, directly or not)
-DEPS = SOURCES + sorted(CSRC.glob("*.h")) + [ROOT / "include" / "psyne_tdt.h"]
+SOURCES = [CSRC / "tdt_api.hip"]  # (diagnostic single-TU builds compile this file alone)
+ENC_WS_SRC = CSRC / "tdt_enc_ws.hip"  # the encode kernels of one word size
+WORD_SIZES = (1, 2, 4, 8, 16)
+# every source and header under csrc/ (tdt_api.hip includes the headers, directly or not)
+DEPS = SOURCES + [ENC_WS_SRC] + sorted(CSRC.glob("*.h")) + [ROOT / "include" / "psyne_tdt.h"]
+OBJ_DIR = PKG / "build"
 
 
 def needs_build() -> bool:
@@ -30,12 +33,27 @@ def needs_build() -> bool:
 
 
 def build(force: bool = False, verbose: bool = False) -> pathlib.Path:
+    """Compile tdt_api.hip and one tdt_enc_ws.hip object per word size in parallel (the encode
+    kernels dominate the compile time), then link libpsyne_tdt.so."""
     if force or needs_build():
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-               "-I", str(ROOT / "include"), *map(str, SOURCES), "-o", str(LIB)]
+        OBJ_DIR.mkdir(exist_ok=True)
+        base = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-I", str(ROOT / "include")]
+        jobs = [(base + ["-c", str(SOURCES[0]), "-o", str(OBJ_DIR / "tdt_api.o")], OBJ_DIR / "tdt_api.o")]
+        for ws in WORD_SIZES:
+            o = OBJ_DIR / f"tdt_enc_ws{ws}.o"
+            jobs.append((base + [f"-DPSY_INST_WS={ws}", "-c", str(ENC_WS_SRC), "-o", str(o)], o))
+        procs = []
+        for cmd, _ in jobs:
+            if verbose:
+                print(" ".join(cmd), flush=True)
+            procs.append(subprocess.Popen(cmd))
+        bad = [cmd for (cmd, _), p in zip(jobs, procs) if p.wait() != 0]
+        if bad:
+            raise subprocess.CalledProcessError(1, bad[0])
+        link = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *(str(o) for _, o in jobs), "-o", str(LIB)]
         if verbose:
-            print(" ".join(cmd), flush=True)
-        subprocess.check_call(cmd)
+            print(" ".join(link), flush=True)
+        subprocess.check_call(link)
     return LIB
 
 

@@ -20,6 +20,21 @@
 #include "tdt_encode.h"
 #include "tdt_slots.h"
 
+// The encode kernels live in tdt_enc_ws.hip (one translation unit per word size); diagnostic
+// builds (word size 4 only, phase profiling) instantiate them here instead.
+#if !defined(PSY_FAST_BUILD) && !(defined(PSY_PROF) && PSY_PROF) && !defined(PSY_SINGLE_TU)
+#define PSY_ENC_EXT(WS, T, G, M, L, TL) \
+    extern template __global__ void psy::tdt_encode_kernel<WS, T, G, psy::M, L, TL>(psy::EncodeArgs);
+#define PSY_ENC_EXT_WS(WS)                 \
+    PSY_ENC_INSTANCES(PSY_ENC_EXT, WS)     \
+    extern template __global__ void psy::tdt_encode_lscan_kernel<WS>(psy::EncodeArgs, const uint32_t *, uint32_t);
+PSY_ENC_EXT_WS(1)
+PSY_ENC_EXT_WS(2)
+PSY_ENC_EXT_WS(4)
+PSY_ENC_EXT_WS(8)
+PSY_ENC_EXT_WS(16)
+#endif
+
 namespace {
 
 thread_local std::string g_err;

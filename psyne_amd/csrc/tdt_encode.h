@@ -45,8 +45,8 @@
 
 namespace psy {
 
-__constant__ __attribute__((aligned(16))) double c_log2_tab[128] = PSY_LOG2_TAB_INIT;
-__constant__ __attribute__((aligned(16))) double c_log2_tab2[128] = PSY_LOG2_TAB2_INIT;
+static __constant__ __attribute__((aligned(16))) double c_log2_tab[128] = PSY_LOG2_TAB_INIT;
+static __constant__ __attribute__((aligned(16))) double c_log2_tab2[128] = PSY_LOG2_TAB2_INIT;
 
 enum { MODE_ENCODE = 0, MODE_MAPPED = 1, MODE_ANALYZE = 2 };
 
@@ -1421,6 +1421,7 @@ struct PlanArgs {
 
 constexpr uint32_t kPlanThreads = 1024, kPlanPer = 2;  // messages per plan workgroup: 2048
 
+#ifndef PSY_ENC_INST_TU  // (defined once, in tdt_api.hip)
 __global__ __launch_bounds__(kPlanThreads) void tdt_encode_plan_kernel(PlanArgs p) {
     __shared__ uint64_t lds[kPlanPer * 16 + 1];
     const uint32_t scap = p.tile_cap / kSpanTiles;
@@ -1472,6 +1473,8 @@ __global__ __launch_bounds__(kPlanThreads) void tdt_encode_plan_kernel(PlanArgs 
         if (md[k]) p.mlist[pm[k]] = i;
     }
 }
+
+#endif  // PSY_ENC_INST_TU
 
 // Large messages, between the count and emit passes: one wave per message walks its tile
 // records in order — prefix max of the last run start (the run carried into each tile),
@@ -1559,5 +1562,14 @@ __global__ __launch_bounds__(64) void tdt_encode_lscan_kernel(EncodeArgs a, cons
         }
     }
 }
+
+// The kernel instances of one word size.  The product library instantiates them in
+// tdt_enc_ws.hip, one translation unit per word size (compiled in parallel), and tdt_api.hip
+// declares them extern; diagnostic single-TU builds instantiate them implicitly.
+#define PSY_ENC_INSTANCES(X, WS)                                                                      \
+    X(WS, 512, 8, MODE_ENCODE, 0, 0) X(WS, 512, 8, MODE_ENCODE, 0, 1) X(WS, 512, 8, MODE_ENCODE, 0, 2) \
+    X(WS, 512, 8, MODE_ENCODE, 0, 3) X(WS, 512, 8, MODE_ENCODE, 0, 4) X(WS, 64, 4, MODE_ENCODE, 0, 0)  \
+    X(WS, 64, 4, MODE_ENCODE, 1, 0) X(WS, 512, 8, MODE_ENCODE, 1, 0) X(WS, 64, 4, MODE_MAPPED, 1, 0)   \
+    X(WS, 512, 8, MODE_MAPPED, 1, 0) X(WS, 64, 4, MODE_ANALYZE, 1, 0) X(WS, 512, 8, MODE_ANALYZE, 1, 0)
 
 }  // namespace psy
