@@ -382,6 +382,7 @@ int encode_common(tdt_ctx *c, int mode, const uint8_t *d_in, const uint64_t *d_i
 // passes (tdt_decode.h).  Grids are sized from the plan's counts (read back; conservative
 // under stream capture, where every blob takes the one-wave path).
 constexpr uint32_t kDLmax = 1u << 16, kDBcap = 1u << 23, kDTcap = 1u << 20;
+constexpr uint64_t kDSmallMax = 1024;  // decoded sizes up to one window of one round
 size_t dlarge_bytes() {
     return (size_t)kDLmax * sizeof(psy::DMeta) + 8ull * kDBcap + 4ull * kDTcap + 8ull * kDTcap;
 }
@@ -399,20 +400,23 @@ int launch_decode_slotted(tdt_ctx *c, PlanWS &pw, psy::DecodeArgs a, hipStream_t
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     HIPCHK(hipStreamIsCapturing(s, &cap));
     const bool capturing = cap != hipStreamCaptureStatusNone;
-    HIPCHK(hipMemsetAsync(cnt, 0, 32, s));
-    psy::DPlanArgs p{a.in, a.in_off, a.in_len, n, cnt, list, dmeta, bent, tent, kDLmax, kDBcap, kDTcap,
-                     capturing ? ~0ull : c->large_min};
+    HIPCHK(hipMemsetAsync(cnt, 0, 40, s));
+    uint32_t *slist = list + n;
+    // (under stream capture the counts cannot be read back: every blob then takes the one list)
+    psy::DPlanArgs p{a.in, a.in_off, a.in_len, n, cnt, list, slist, capturing ? 0 : kDSmallMax, dmeta, bent, tent,
+                     kDLmax, kDBcap, kDTcap, capturing ? ~0ull : c->large_min};
     hipLaunchKernelGGL(psy::tdt_decode_plan_kernel, dim3((uint32_t)(((uint64_t)n + 4095) / 4096)), dim3(1024), 0, s, p);
     HIPCHK(hipGetLastError());
-    uint32_t nn = n, nl = 0, nb = 0, nt = 0;
+    uint32_t nn = n, nl = 0, nb = 0, nt = 0, ns = 0;
     if (!capturing) {
-        HIPCHK(hipMemcpyAsync(pw.host, cnt, 32, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(pw.host, cnt, 40, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
         const uint64_t *h = reinterpret_cast<const uint64_t *>(pw.host);
         nn = (uint32_t)h[0];
         nl = (uint32_t)std::min<uint64_t>(h[1], kDLmax);
         nt = (uint32_t)std::min<uint64_t>(h[2], kDTcap);
         nb = (uint32_t)std::min<uint64_t>(h[3], kDBcap);
+        ns = (uint32_t)h[4];
     }
     a.list = list;
     a.dmeta = dmeta;
@@ -430,6 +434,12 @@ int launch_decode_slotted(tdt_ctx *c, PlanWS &pw, psy::DecodeArgs a, hipStream_t
     launch_list(nn, 64, [&](uint32_t b, uint32_t g) {
         a.list_base = b;
         hipLaunchKernelGGL((psy::tdt_decode_kernel<0>), dim3(g), dim3(64), 0, s, a);
+    });
+    // small blobs: one-round windows (a third less LDS per wave: more blobs in flight per CU)
+    a.list = slist;
+    launch_list(ns, 64, [&](uint32_t b, uint32_t g) {
+        a.list_base = b;
+        hipLaunchKernelGGL((psy::tdt_decode_kernel<0, 1>), dim3(g), dim3(64), 0, s, a);
     });
     return TDT_OK;
 }

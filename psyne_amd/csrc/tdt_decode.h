@@ -63,9 +63,10 @@ constexpr uint32_t kDecTileGroups = 2048;  // large blobs: 32 KiB of output per 
 constexpr int kDecWR = PSY_DEC_WR;  // rounds per window
 constexpr int kHdrCache = 256;
 
-struct DecLayout {
+template <int WR = kDecWR>
+struct DecLayoutT {
     // heads: sum_r (WR·64·WPG·k_r + 16 pad) u16 <= WR·1024 + 16·16 entries
-    static constexpr int HEADS = (kDecWR * 1024 + 16 * kMaxRef) * 2;
+    static constexpr int HEADS = (WR * 1024 + 16 * kMaxRef) * 2;
     static constexpr int PLANES = 1024 + 64;  // one round of plane bytes (+ slack)
     static constexpr int HDR = kHdrCache + 16;
     static constexpr int MISC = 256 * 4;
@@ -75,6 +76,7 @@ struct DecLayout {
     static constexpr int OFF_MISC = OFF_HDR + HDR;
     static constexpr int BYTES = OFF_MISC + MISC;
 };
+using DecLayout = DecLayoutT<>;
 
 // misc (uint32 index)
 enum {
@@ -194,7 +196,6 @@ __global__ __launch_bounds__(256) void tdt_decode_sizes_kernel(DecodeArgs a) {
 // seeded by a wave max-scan of each lane's last head (restricted to its own stream) or by the
 // stream's carry, gives every position its run's value.  Planes → LDS; each lane gathers its
 // group's segments (dword reads) and v_perm's them into word order (recombine :614-637).
-constexpr int kFastWR = kDecWR;
 
 // Parameters of a fast-path blob (parse_fast): referenced streams r = 0, 1 (stream 1 absent
 // when !two) with seg[r] = WPG·k_r bytes per 16-byte group, np[r] pairs at blob offset soff[r].
@@ -210,11 +211,12 @@ struct FastHdr {
 // starts inside the blob begins at block b0[r] of stream r — the 512-pair block holding
 // position g_lo·seg_r - 1, whose first pair starts at s0[r] (the scan's prefix); kNone: the
 // stream ends before the tile (s0 = its length).
+template <int WR_ = kDecWR>
 __device__ __forceinline__ void decode_fast(const FastHdr &H, uint8_t *smem, const uint8_t *blob, const uint8_t *blim,
                                             uint8_t *dst, uint32_t ngroups, uint64_t wbytes, uint32_t g_lo = 0,
                                             uint32_t g_hi = 0, const uint32_t *b0 = nullptr, const uint32_t *s0 = nullptr) {
-    using Lay = DecLayout;
-    constexpr uint32_t WR = kFastWR;
+    using Lay = DecLayoutT<WR_>;
+    constexpr uint32_t WR = WR_;
     const uint32_t lane = (uint32_t)lane_id();
     PSY_PROF_BEGIN();
     uint16_t *heads = reinterpret_cast<uint16_t *>(smem + Lay::OFF_HEADS);
@@ -533,9 +535,9 @@ __device__ __forceinline__ FastHdr parse_fast(const uint8_t *blob, uint64_t len,
 }
 
 // One blob, one wave (LB: compacted output by look-back; else its slot).
-template <int LB>
+template <int LB, int WR = kDecWR>
 __device__ __forceinline__ void decode_one(const DecodeArgs &a, uint8_t *smem, uint32_t msg) {
-    using Lay = DecLayout;
+    using Lay = DecLayoutT<WR>;
     uint32_t *misc = reinterpret_cast<uint32_t *>(smem + Lay::OFF_MISC);
     uint8_t *hdrc = smem + Lay::OFF_HDR;
     const int lane = lane_id();
@@ -595,7 +597,7 @@ __device__ __forceinline__ void decode_one(const DecodeArgs &a, uint8_t *smem, u
         const uint64_t wbytes = (uint64_t)(H.orig / H.ws) * H.ws;
         // recombine :617 zero-initialises; bytes past the last whole word stay zero
         if (H.orig > wbytes) team_zero<64>(dst + wbytes, H.orig - wbytes);
-        decode_fast(H, smem, blob, blim, dst, (uint32_t)((wbytes + 15) / 16), wbytes);
+        decode_fast<WR>(H, smem, blob, blim, dst, (uint32_t)((wbytes + 15) / 16), wbytes);
         return;
     }
     auto rd32 = [&](uint64_t off) -> uint32_t {
@@ -653,7 +655,7 @@ __device__ __forceinline__ void decode_one(const DecodeArgs &a, uint8_t *smem, u
                     for (uint32_t u = 0; u < seg; ++u) misc[D_SB + soffb + u] = (r << 8) | u;
                     if (seg & 3u) fast = 0;
                     soffb += seg;
-                    hoff += kDecWR * 64 * seg + 16;
+                    hoff += WR * 64 * seg + 16;
                     pb += 64 * seg;
                 }
                 misc[D_FAST] = fast;
@@ -775,7 +777,7 @@ __device__ __forceinline__ void decode_one(const DecodeArgs &a, uint8_t *smem, u
     uint4 pf0 = make_uint4(0, 0, 0, 0), pf1 = make_uint4(0, 0, 0, 0);
     uint32_t pf_idx0 = ~0u, pf_idx1 = ~0u;
 
-    for (uint32_t gwin = 0; gwin < ngroups; gwin += 64 * kDecWR) {
+    for (uint32_t gwin = 0; gwin < ngroups; gwin += 64 * WR) {
         // ---- zero the heads of this window (16 B per lane per step)
         for (uint32_t i = (uint32_t)lane; i < (uint32_t)Lay::HEADS / 16; i += 64)
             reinterpret_cast<uint4 *>(heads)[i] = make_uint4(0, 0, 0, 0);
@@ -789,7 +791,7 @@ __device__ __forceinline__ void decode_one(const DecodeArgs &a, uint8_t *smem, u
             uint32_t pidx = __builtin_amdgcn_readfirstlane(misc[D_PIDX + r]);
             uint32_t pos = __builtin_amdgcn_readfirstlane(misc[D_POS + r]);
             const uint32_t wstart = gwin * WPG * k;
-            const uint32_t wlen = kDecWR * 64 * WPG * k;
+            const uint32_t wlen = WR * 64 * WPG * k;
             const uint32_t hb = Lay::OFF_HEADS + 2u * hoff;
             while (pidx < np && pos - wstart < wlen) {
                 const uint32_t p0 = pidx + 8u * (uint32_t)lane;
@@ -859,7 +861,7 @@ __device__ __forceinline__ void decode_one(const DecodeArgs &a, uint8_t *smem, u
         team_sync<1>();
         PSY_PROF_MARK(9);
         // ---- per round: fill the planes, recombine, store
-        for (uint32_t rl = 0; rl < (uint32_t)kDecWR; ++rl) {
+        for (uint32_t rl = 0; rl < (uint32_t)WR; ++rl) {
             const uint32_t g0 = gwin + rl * 64;
             if (g0 >= ngroups) break;
             // lane's 16 plane positions: heads[hoff + rl·64·WPG·k + fu ..)
@@ -955,8 +957,10 @@ struct DPlanArgs {
     const uint64_t *in_off;
     const uint64_t *in_len;
     uint32_t n_msgs;
-    unsigned long long *cnt;  // [0] one-wave blobs, [1] large blobs, [2] tiles, [3] block slots
+    unsigned long long *cnt;  // [0] one-wave blobs, [1] large blobs, [2] tiles, [3] block slots, [4] small blobs
     uint32_t *list;
+    uint32_t *slist;          // blobs decoding to <= small_max bytes (one-round windows: less LDS per wave)
+    uint64_t small_max;
     DMeta *dmeta;
     uint32_t *bent, *tent;
     uint32_t lmax, bcap, tcap;
@@ -973,11 +977,13 @@ __global__ __launch_bounds__(1024) void tdt_decode_plan_kernel(DPlanArgs p) {
         const uint64_t share = (last - p.in_off[0]) / 4096;
         thr = share > thr ? share : thr;
     }
-    uint64_t isl[4], nt[4], nb[4], j[4], t0[4], b0[4], one[4], pos[4];
+    uint64_t isl[4], nt[4], nb[4], j[4], t0[4], b0[4], one[4], pos[4], sm[4], spos[4];
+    uint64_t osz_k[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const uint32_t i = (blockIdx.x * 4 + k) * 1024 + threadIdx.x;
         isl[k] = nt[k] = nb[k] = 0;
+        osz_k[k] = 0;
         if (i < p.n_msgs) {
             const uint64_t boff = p.in_off[i];
             const uint64_t len = p.in_len ? p.in_len[i] : p.in_off[i + 1] - boff;
@@ -991,6 +997,7 @@ __global__ __launch_bounds__(1024) void tdt_decode_plan_kernel(DPlanArgs p) {
                     osz = len - 4;
                 }
             }
+            osz_k[k] = osz;
             if (osz > thr) {
                 isl[k] = 1;
                 nt[k] = (osz + 16ull * kDecTileGroups - 1) / (16ull * kDecTileGroups);
@@ -1021,12 +1028,17 @@ __global__ __launch_bounds__(1024) void tdt_decode_plan_kernel(DPlanArgs p) {
                 for (uint64_t b = b0[k]; b < b0[k] + nb[k] && b < p.bcap; ++b) p.bent[b] = kNone;
             }
         }
-        one[k] = (i < p.n_msgs && !large) ? 1u : 0u;
+        const bool any = i < p.n_msgs && !large;
+        sm[k] = (any && p.small_max && osz_k[k] <= p.small_max) ? 1u : 0u;
+        one[k] = (any && !sm[k]) ? 1u : 0u;
     }
     wg_claim<4>(one, pos, p.cnt, lds);
+    wg_claim<4>(sm, spos, p.cnt + 4, lds);
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
+    for (int k = 0; k < 4; ++k) {
         if (one[k]) p.list[pos[k]] = (blockIdx.x * 4 + k) * 1024 + threadIdx.x;
+        if (sm[k]) p.slist[spos[k]] = (blockIdx.x * 4 + k) * 1024 + threadIdx.x;
+    }
 }
 
 // Prep: one workgroup per large blob; wave 0 parses and places it, then every thread writes
@@ -1191,9 +1203,9 @@ __global__ __launch_bounds__(64) void tdt_decode_ltile_kernel(DecodeArgs a) {
 
 // Blob ids: the look-back needs them in dispatch order (atomic ticket); slotted batches take
 // them from the plan's list (or, without one, the workgroup id).
-template <int LB>
+template <int LB, int WR = kDecWR>
 __global__ __launch_bounds__(64) void tdt_decode_kernel(DecodeArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t smem[DecLayout::BYTES];
+    __shared__ __attribute__((aligned(16))) uint8_t smem[DecLayoutT<WR>::BYTES];
     uint32_t msg;
     if constexpr (LB) {
         uint32_t t = 0;
@@ -1202,7 +1214,7 @@ __global__ __launch_bounds__(64) void tdt_decode_kernel(DecodeArgs a) {
     } else {
         msg = a.list ? a.list[a.list_base + blockIdx.x] : a.list_base + blockIdx.x;
     }
-    decode_one<LB>(a, smem, msg);
+    decode_one<LB, WR>(a, smem, msg);
 }
 
 }  // namespace psy

@@ -70,10 +70,11 @@ struct ScanIdem {
 template <class Op>
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
     if constexpr (ScanIdem<Op>::value) {
-        x = Op::f(x, dpp_mov_self<0x111>(x));
-        x = Op::f(x, dpp_mov_self<0x112>(x));
-        x = Op::f(x, dpp_mov_self<0x114>(x));
-        x = Op::f(x, dpp_mov_self<0x118>(x));
+        // row shifts with bound_ctrl (out-of-row lanes read 0, the identity): one v_mov_dpp each
+        x = Op::f(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true));
+        x = Op::f(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, true));
+        x = Op::f(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, true));
+        x = Op::f(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true));
         x = Op::f(x, dpp_mov_self<0x142, 0xa>(x));
         x = Op::f(x, dpp_mov_self<0x143, 0xc>(x));
         return x;
@@ -117,10 +118,8 @@ __device__ __forceinline__ uint32_t pk_sub_u16(uint32_t a, uint32_t b) {
 struct OpPkMax {
     __device__ __forceinline__ static uint32_t f(uint32_t a, uint32_t b) { return pk_max_u16(a, b); }
 };
-template <>
-struct ScanIdem<OpMax> {
-    static constexpr bool value = true;
-};
+// (OpMax takes the identity-0 path: the compiler folds each DPP move into v_max_u32_dpp, one
+// VALU per step; v_pk_max_u16 has no DPP form, so OpPkMax keeps the self-identity moves.)
 template <>
 struct ScanIdem<OpPkMax> {
     static constexpr bool value = true;

@@ -140,8 +140,10 @@ struct EncLayout {
     static constexpr int TERMS = TEAM >= 256 ? TB * 256 * 16 : 0;  // one-wave teams: in registers
     // Two phases share one region: histogram + entropy terms + log2 tables (dead once the
     // mapping is known) and pass B's per-wave staging windows.
-    // + log2 tables (2 KiB) + the per-message term table for counts 1..64 (1 KiB)
-    static constexpr int ANALYSIS = HISTA + TERMS + 2048 + 1024;
+    // + log2 tables (2 KiB) + the per-message term table for counts 1..64 (1 KiB); one-wave
+    // teams read the tables from constant memory and keep the term table in registers (their
+    // LDS footprint sets how many messages a CU holds)
+    static constexpr int ANALYSIS = HISTA + TERMS + (TEAM >= 256 ? 2048 + 1024 : 0);
     static constexpr int REGION = STAGE > ANALYSIS ? STAGE : ANALYSIS;
     static constexpr int SLOTS = W * 8 * 4;
     static constexpr int MISC = 512;
@@ -198,7 +200,7 @@ __device__ __forceinline__ uint32_t spread2(uint32_t e) {
 #ifndef PSY_ENC_WPE
 #define PSY_ENC_WPE 6
 #endif
-#define PSY_ENC_WAVES(TEAM) ((TEAM) >= 512 ? PSY_ENC_WPE : 1)
+#define PSY_ENC_WAVES(TEAM) ((TEAM) >= 512 ? PSY_ENC_WPE : 7)
 
 // One message — or, TL > 0, part of a large message: TL 1 the histogram of one span of
 // kSpanTiles tiles (UNCP messages: the span's copy), 4 the mapping from the message's span
@@ -342,9 +344,9 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
     // glibc log2 tables for the entropy pass, fetched BEFORE the message's rounds so that the
     // LDS copy below waits for these loads only (issued after the rounds, its wait would
     // cover every round's load and stall the team until the whole message had arrived)
-    constexpr int NL2 = (128 + TEAM - 1) / TEAM;
+    constexpr int NL2 = W == 1 ? 1 : (128 + TEAM - 1) / TEAM;
     uint4 l2v[NL2];
-    if constexpr (MODE != MODE_MAPPED) {
+    if constexpr (MODE != MODE_MAPPED && W > 1) {
 #pragma unroll
         for (int k = 0; k < NL2; ++k) {
             const int i = (tid + k * TEAM) & 127;
@@ -421,9 +423,11 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
             }
         }
         // glibc log2 tables → LDS (the bins' log2 evaluations read them with per-lane indices)
+        if constexpr (W > 1) {
 #pragma unroll
-        for (int k = 0; k < NL2; ++k)
-            if (tid + k * TEAM < 128) reinterpret_cast<uint4 *>(smem + Lay::OFF_LOG2)[tid + k * TEAM] = l2v[k];
+            for (int k = 0; k < NL2; ++k)
+                if (tid + k * TEAM < 128) reinterpret_cast<uint4 *>(smem + Lay::OFF_LOG2)[tid + k * TEAM] = l2v[k];
+        }
         team_sync<W>();
         const uint32_t zoff = (uint32_t)lane * 4u;
         const uint32_t coff = (64u + ((uint32_t)lane & (Lay::HC - 1))) * 4u;
@@ -476,34 +480,57 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
         // needs no select: fma(0, 0, e) == e for the non-negative running sum); then in every
         // wave one lane per position runs the exact fma chain in bin order.
         double *terms = reinterpret_cast<double *>(smem + Lay::OFF_TERMS);
-        const double *ltab = reinterpret_cast<const double *>(smem + Lay::OFF_LOG2);
+        const double *ltab = W == 1 ? c_log2_tab : reinterpret_cast<const double *>(smem + Lay::OFF_LOG2);
+        const double *ltab2 = W == 1 ? c_log2_tab2 : ltab + 128;
         const double total = (double)wc;
         // Counts repeat: the terms of counts 1..64 are computed once per message (exactly the
-        // operations below, so the same bits) and looked up; larger counts are computed.
+        // operations below, so the same bits) and looked up; larger counts are computed.  Lane i
+        // holds count i + 1's terms (one-wave teams: in registers, looked up by ds_bpermute).
         double *ctab = reinterpret_cast<double *>(smem + Lay::OFF_CTAB);
+        double c_np = 0.0, c_L = 0.0;
         if (tid < 64) {
             double prob;
             {
 #pragma clang fp contract(off)
                 prob = (double)(uint32_t)(tid + 1) / total;
-                ctab[2 * tid + 1] = psy_log2_glibc(prob, ltab, ltab + 128);
+                c_L = psy_log2_glibc(prob, ltab, ltab2);
             }
-            ctab[2 * tid] = -prob;
+            c_np = -prob;
+            if constexpr (W > 1) {
+                ctab[2 * tid] = c_np;
+                ctab[2 * tid + 1] = c_L;
+            }
         }
         team_sync<W>();
         // (-prob, log2 prob) of a bin with count c
+        auto shfl_f64 = [&](double x, uint32_t src) __attribute__((always_inline)) -> double {
+            const uint64_t u = __builtin_bit_cast(uint64_t, x);
+            const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)(uint32_t)u);
+            const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)(uint32_t)(u >> 32));
+            return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+        };
         auto bin_terms = [&](uint32_t c, double &np, double &L) __attribute__((always_inline)) {
             np = 0.0;
             L = 0.0;
+            if constexpr (W == 1) {
+                // every lane takes part in the permutes (counts 0 and > 64 read lane 0 and
+                // are then overwritten / ignored)
+                const uint32_t src = c - 1u <= 63u ? c - 1u : 0u;
+                const double tnp = shfl_f64(c_np, src), tL = shfl_f64(c_L, src);
+                if (c - 1u <= 63u) {
+                    np = tnp;
+                    L = tL;
+                }
+            }
             if (c > 64u) {
                 double prob;
                 {
 #pragma clang fp contract(off)
                     prob = (double)c / total;
-                    L = psy_log2_glibc(prob, ltab, ltab + 128);
+                    L = psy_log2_glibc(prob, ltab, ltab2);
                 }
                 np = -prob;
-            } else if (c) {
+            } else if (W > 1 && c) {
                 const double2 t = reinterpret_cast<const double2 *>(ctab)[c - 1];
                 np = t.x;
                 L = t.y;
