@@ -155,9 +155,10 @@ int launch_encode_t(psy::EncodeArgs a, hipStream_t s) {
 // workgroups exit at once) and large messages stay medium.
 constexpr uint64_t kSmallMax = 4096;  // one-wave teams up to this size
 constexpr uint32_t kLmax = 1u << 16;   // large messages per batch
-// tiles per batch: 64 MiB of span histograms (WS KiB per 512 KiB span) — 8 GiB of large
-// messages at word size 4; further large messages in the batch stay medium
-uint32_t tile_cap_of(int ws) { return (65536u / (uint32_t)ws) * psy::kSpanTiles; }
+// tiles per batch: 256 MiB of span histograms (WS KiB per 512 KiB span) — 32 GiB of large
+// messages at word size 4 (C4's 4 Mi-message Zipf batch holds 12 GiB of them); further large
+// messages in the batch stay medium (one 512-lane team each, streaming: far slower)
+uint32_t tile_cap_of(int ws) { return (262144u / (uint32_t)ws) * psy::kSpanTiles; }
 size_t large_bytes(int ws) {
     const size_t tc = tile_cap_of(ws);
     return (size_t)kLmax * sizeof(psy::LMeta) + tc * (8 + sizeof(psy::TileRec)) + (tc / psy::kSpanTiles) * 8 +
