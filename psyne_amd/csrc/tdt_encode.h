@@ -120,12 +120,15 @@ template <int WS, int TEAM>
 struct EncLayout {
     static constexpr int W = TEAM / 64;
     static constexpr int WPG = 16 / WS;  // words per 16-byte group
-    // histogram, per byte position: [64 per-lane zero bins][256 bins x HC copies] (uint32)
+    // histogram, per byte position (uint32): bins 1..255 x HC copies (bin v copy k at
+    // (v - 1)·HC + k), one unused row, then 64 per-lane zero bins at ZB + lane.
     // 16 KiB of copies whatever the word size for message-sized teams; one copy for the
     // one-wave small-message kernel (its LDS footprint sets how many messages a CU holds)
     static constexpr int HC = TEAM >= 256 ? 16 / WS : 1;
     static constexpr int LOG_HC = HC == 1 ? 0 : HC == 2 ? 1 : HC == 4 ? 2 : HC == 8 ? 3 : 4;
+    static constexpr int ZB = 256 * HC;
     static constexpr int PS = 64 + 256 * HC;
+    static constexpr int bin(int v, int k) { return (v - 1) * HC + k; }  // v >= 1
     static constexpr int HIST = WS * PS * 4;
     static constexpr int HISTA = HIST;
     static constexpr int TB = (TEAM >= 256) ? (WS < 4 ? WS : 4) : 1;
@@ -419,7 +422,8 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
             for (int i = tid; i < WS * 256; i += TEAM) {
                 uint32_t c = 0;
                 for (uint32_t k = 0; k < nsp; ++k) c += sh[(uint64_t)k * WS * 256 + i];
-                hist[(i >> 8) * Lay::PS + 64 + (i & 255) * Lay::HC] = c;
+                const int v = i & 255;
+                hist[(i >> 8) * Lay::PS + (v ? Lay::bin(v, 0) : Lay::ZB)] = c;
             }
         }
         // glibc log2 tables → LDS (the bins' log2 evaluations read them with per-lane indices)
@@ -429,14 +433,17 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
                 if (tid + k * TEAM < 128) reinterpret_cast<uint4 *>(smem + Lay::OFF_LOG2)[tid + k * TEAM] = l2v[k];
         }
         team_sync<W>();
-        const uint32_t zoff = (uint32_t)lane * 4u;
-        const uint32_t coff = (64u + ((uint32_t)lane & (Lay::HC - 1))) * 4u;
+        // Compare-free bin address: v·4HC + 4(copy - HC) is bin v's copy for v >= 1 and wraps
+        // to >= 2^32 - 4HC for v = 0, so min() with this lane's zero bin (above every bin)
+        // selects it — 3 VALU per byte (bfe, lshl_add, min), no compare / vcc / select.
+        const uint32_t zoff = (uint32_t)(Lay::ZB + lane) * 4u;
+        const uint32_t coff = (((uint32_t)lane & (Lay::HC - 1)) - (uint32_t)Lay::HC) * 4u;
         auto hist_group = [&](const uint4 &d, uint32_t vb, bool full) __attribute__((always_inline)) {
             const uint32_t dw[4] = {d.x, d.y, d.z, d.w};
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
                 const uint32_t v = (dw[i >> 2] >> (8 * (i & 3))) & 0xffu;
-                const uint32_t ad = v ? (v << (Lay::LOG_HC + 2)) + coff : zoff;
+                const uint32_t ad = umin((v << (Lay::LOG_HC + 2)) + coff, zoff);
 #ifndef PSY_X_NOHIST
                 if (full || (uint32_t)i < vb)
 #else
@@ -460,9 +467,9 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
                 const int b = i >> 8, v = i & 255;
                 uint32_t c = 0;
 #pragma unroll
-                for (int k = 0; k < Lay::HC; ++k) c += hist[b * Lay::PS + 64 + v * Lay::HC + k];
+                for (int k = 0; k < Lay::HC; ++k) c += v ? hist[b * Lay::PS + Lay::bin(v, k)] : 0u;
                 if (v == 0)
-                    for (int z = 0; z < 64; ++z) c += hist[b * Lay::PS + z];
+                    for (int z = 0; z < 64; ++z) c += hist[b * Lay::PS + Lay::ZB + z];
                 sh[i] = c;
             }
             return;
@@ -471,7 +478,7 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
         auto count = [&](int b, int v) __attribute__((always_inline)) -> uint32_t {
             uint32_t c = 0;
 #pragma unroll
-            for (int k = 0; k < Lay::HC; ++k) c += hist[b * Lay::PS + 64 + v * Lay::HC + k];
+            for (int k = 0; k < Lay::HC; ++k) c += v ? hist[b * Lay::PS + Lay::bin(v, k)] : 0u;
             return c;
         };
 
@@ -567,7 +574,7 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
                     if (v >= 256) break;  // wave-uniform
                     uint32_t c = count(b, v);
                     if (v < 64) {  // wave-uniform: bin 0 adds the 64 per-lane zero bins
-                        const uint32_t z = wave_reduce<OpAdd>(hist[b * Lay::PS + lane]);
+                        const uint32_t z = wave_reduce<OpAdd>(hist[b * Lay::PS + Lay::ZB + lane]);
                         if (lane == 0) c += z;
                     }
                     double np, L;
@@ -612,7 +619,7 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
                 if (b < WS) {
                     uint32_t c = count(b, i & 255);
                     if ((i & 255) < 64) {  // wave-uniform: bin 0 adds the 64 per-lane zero bins
-                        const uint32_t z = wave_reduce<OpAdd>(hist[b * Lay::PS + lane]);
+                        const uint32_t z = wave_reduce<OpAdd>(hist[b * Lay::PS + Lay::ZB + lane]);
                         if (lane == 0) c += z;
                     }
                     if constexpr (MODE == MODE_ANALYZE) {
@@ -1245,6 +1252,18 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
         uint32_t pend6[2] = {0, 0};
 #pragma unroll
         for (int c = 0; c < 2; ++c) pend6[c] = ((pend[c] >> 24) << 8) | ((pend[c] - 256u + gw0 * Ls[c]) & 0xffu);
+        // slot 4t + q's stream position mod 256 in byte t of pos6[q] (rounds start at multiples
+        // of 256 positions, so these are round-invariant)
+        uint32_t pos6[4] = {0, 0, 0, 0};
+        if constexpr (E6) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const uint32_t j = 4u * t + q;
+                    pos6[q] |= (((j < L0 ? pb0 : pb1) + j) & 0xffu) << (8 * t);
+                }
+        }
         auto sweep6 = [&](const uint4 &Tw, uint32_t C) __attribute__((always_inline)) {
             PSY_ASM_ROUND(B);
             const uint32_t T[4] = {Tw.x, Tw.y, Tw.z, Tw.w};
@@ -1256,6 +1275,13 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
             const uint32_t D0 = eb6 + 2u * (1u + s6[0] + (pexc & 0xffffu)) - jl;
             const uint32_t D1 = eb6 + eoff6 + 2u * (1u + s6[1] + (pexc >> 16)) - jl;
             uint32_t D = L0 == 0 ? D1 : D0;
+            // entries of slots q + 4t, two per dword: E[q][0] = slots q, q+4; E[q][1] = q+8, q+12
+            uint32_t E[4][2];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                E[q][0] = perm(T[q], pos6[q], 0x05010400u);
+                E[q][1] = perm(T[q], pos6[q], 0x07030602u);
+            }
 #pragma unroll
             for (int j = 0; j < 16; ++j) {
                 const int q = j & 3, t = j >> 2;
@@ -1263,8 +1289,9 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
                 const uint32_t bit = (C >> j) & 1u;
                 uint32_t ad;
                 asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(ad) : "v"(bit), "v"(D), "v"(jl));
-                const uint32_t pos = ((uint32_t)j < L0 ? pb0 : pb1) + (uint32_t)j;
-                *reinterpret_cast<uint16_t *>(smem + ad) = (uint16_t)perm(T[q], pos, 0x0c0c0000u | ((uint32_t)(4 + t) << 8));
+                const uint32_t e = E[q][t >> 1];
+                if (t & 1) *reinterpret_cast<uint16_t *>(smem + ad) = (uint16_t)(e >> 16);
+                else *reinterpret_cast<uint16_t *>(smem + ad) = (uint16_t)e;
                 asm("v_lshl_add_u32 %0, %1, 1, %2" : "=v"(D) : "v"(bit), "v"(D));
             }
             s6[0] += Stot & 0xffffu;
