@@ -65,16 +65,24 @@ constexpr int kHdrCache = 256;
 
 template <int WR = kDecWR>
 struct DecLayoutT {
-    // heads: sum_r (WR·64·WPG·k_r + 16 pad) u16 <= WR·1024 + 16·16 entries
-    static constexpr int HEADS = (WR * 1024 + 16 * kMaxRef) * 2;
+    // Fast path (decode_fast): the two referenced streams' heads, WR·64·seg_r + 16 pad u16 each
+    // (seg_0 + seg_1 = 16); a round's plane bytes are staged inside the heads of that round
+    // (already read by the fill) and zeroed after the gather.
+    static constexpr int FHEADS = (WR * 1024 + 32) * 2;
+    // Generic path (any shape, up to 16 referenced streams): windows of GWR rounds, its own
+    // planes and the lane-0 parser's fields.
+    static constexpr int GWR = 1;
+    static constexpr int GHEADS = (GWR * 1024 + 16 * kMaxRef) * 2;
     static constexpr int PLANES = 1024 + 64;  // one round of plane bytes (+ slack)
-    static constexpr int HDR = kHdrCache + 16;
-    static constexpr int MISC = 256 * 4;
+    static constexpr int MISC = 192 * 4;      // D_* fields
+    // The header cache is read only while the blob's header is parsed, before any heads write.
+    static constexpr int OFF_HDR = 0;
     static constexpr int OFF_HEADS = 0;
-    static constexpr int OFF_PLANES = OFF_HEADS + HEADS;
-    static constexpr int OFF_HDR = OFF_PLANES + PLANES;
-    static constexpr int OFF_MISC = OFF_HDR + HDR;
-    static constexpr int BYTES = OFF_MISC + MISC;
+    static constexpr int OFF_GPLANES = GHEADS;
+    static constexpr int OFF_MISC = OFF_GPLANES + PLANES;
+    static constexpr int GBYTES = OFF_MISC + MISC;
+    static constexpr int BYTES = FHEADS > GBYTES ? FHEADS : GBYTES;
+    static_assert(kHdrCache + 16 <= GHEADS && kHdrCache + 16 <= FHEADS, "header cache inside the heads");
 };
 using DecLayout = DecLayoutT<>;
 
@@ -220,7 +228,6 @@ __device__ __forceinline__ void decode_fast(const FastHdr &H, uint8_t *smem, con
     const uint32_t lane = (uint32_t)lane_id();
     PSY_PROF_BEGIN();
     uint16_t *heads = reinterpret_cast<uint16_t *>(smem + Lay::OFF_HEADS);
-    uint8_t *planes = smem + Lay::OFF_PLANES;
     // (every field is wave-uniform: readfirstlane keeps them in SGPRs)
     auto U = [](uint32_t x) -> uint32_t { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); };
     const bool two = U(H.two) != 0;
@@ -231,6 +238,10 @@ __device__ __forceinline__ void decode_fast(const FastHdr &H, uint8_t *smem, con
     const uint32_t OB[4] = {U(H.OB[0]), U(H.OB[1]), U(H.OB[2]), U(H.OB[3])};
     const uint32_t wlen[2] = {WR * 64u * seg[0], WR * 64u * seg[1]};
     const uint32_t hbase[2] = {(uint32_t)Lay::OFF_HEADS, (uint32_t)Lay::OFF_HEADS + 2u * (wlen[0] + 16u)};
+    // round rl's plane bytes go to the heads of round rl of the stream with the larger segment
+    // (128·seg >= 1 KiB bytes, 16-byte aligned), which the fill has read by then
+    const uint32_t rbig = seg[1] > seg[0] ? 1u : 0u;
+    const uint32_t pl_base = hbase[rbig], pl_step = 128u * seg[rbig];
     // fill lane
     const bool f1 = lane * 16u >= 64u * seg[0];
     const uint32_t fu = f1 ? lane * 16u - 64u * seg[0] : lane * 16u;
@@ -347,7 +358,7 @@ __device__ __forceinline__ void decode_fast(const FastHdr &H, uint8_t *smem, con
         const uint32_t gen = win & 7u;
         if (gen == 0) {
             // (re)initialise the head array every 8 windows
-            for (uint32_t i = lane; i < (uint32_t)Lay::HEADS / 16; i += 64)
+            for (uint32_t i = lane; i < (uint32_t)Lay::FHEADS / 16; i += 64)
                 reinterpret_cast<uint4 *>(heads)[i] = make_uint4(0, 0, 0, 0);
             team_sync<1>();
         }
@@ -371,6 +382,7 @@ __device__ __forceinline__ void decode_fast(const FastHdr &H, uint8_t *smem, con
             const uint32_t g0 = gwin + rl * 64u;
             if (g0 >= g_hi) break;
             const uint32_t hoffb = fh + 2u * rl * 64u * fseg;
+            uint8_t *const planes = smem + pl_base + rl * pl_step;
             // lanes 8-15 of every 16 read their second half first: with 32-byte lane rows the
             // two ds_read_b128 are then bank-conflict-free (MI355X_MICROARCH.md §LDS groups)
             const bool sw = (lane & 8u) != 0u;
@@ -431,12 +443,18 @@ __device__ __forceinline__ void decode_fast(const FastHdr &H, uint8_t *smem, con
             const uint32_t g = g0 + lane;
             if (dal16 && 16ull * (g0 + 64u) <= wbytes) {
                 // a whole aligned round (uniform): one 16-byte store per lane, no per-lane tests
+#ifndef PSY_X_NOSTORE
                 *reinterpret_cast<uint4 *>(dst + 16ull * g) = o;
+#else
+                if (o.x == 0x12345678u && o.y == 0x9abcdef0u) *reinterpret_cast<uint4 *>(dst + 16ull * g) = o;
+#endif
             } else if (g < ngroups) {
                 const uint64_t vb64 = wbytes - 16ull * g;
                 st16_any(dst + 16ull * g, o, vb64 >= 16 ? 16 : (int)vb64);
             }
-            team_sync<1>();  // planes are rewritten by the next round
+            // the planes' bytes are heads slots again: empty for the windows that follow (the
+            // gather's reads precede these writes in the wave's LDS order)
+            *reinterpret_cast<uint4 *>(planes + 16u * lane) = make_uint4(0, 0, 0, 0);
         }
         PSY_PROF_MARK(10);
     }
@@ -655,7 +673,7 @@ __device__ __forceinline__ void decode_one(const DecodeArgs &a, uint8_t *smem, u
                     for (uint32_t u = 0; u < seg; ++u) misc[D_SB + soffb + u] = (r << 8) | u;
                     if (seg & 3u) fast = 0;
                     soffb += seg;
-                    hoff += WR * 64 * seg + 16;
+                    hoff += Lay::GWR * 64 * seg + 16;
                     pb += 64 * seg;
                 }
                 misc[D_FAST] = fast;
@@ -734,8 +752,9 @@ __device__ __forceinline__ void decode_one(const DecodeArgs &a, uint8_t *smem, u
         OA[q] = __builtin_amdgcn_readfirstlane(misc[D_OA + q]);
         OB[q] = __builtin_amdgcn_readfirstlane(misc[D_OB + q]);
     }
+    constexpr uint32_t GWR = Lay::GWR;
     uint16_t *heads = reinterpret_cast<uint16_t *>(smem + Lay::OFF_HEADS);
-    uint8_t *planes = smem + Lay::OFF_PLANES;
+    uint8_t *planes = smem + Lay::OFF_GPLANES;
 
     // (blobs parse_fast accepts never get here; the generic path serves every other shape)
 
@@ -777,9 +796,9 @@ __device__ __forceinline__ void decode_one(const DecodeArgs &a, uint8_t *smem, u
     uint4 pf0 = make_uint4(0, 0, 0, 0), pf1 = make_uint4(0, 0, 0, 0);
     uint32_t pf_idx0 = ~0u, pf_idx1 = ~0u;
 
-    for (uint32_t gwin = 0; gwin < ngroups; gwin += 64 * WR) {
+    for (uint32_t gwin = 0; gwin < ngroups; gwin += 64 * GWR) {
         // ---- zero the heads of this window (16 B per lane per step)
-        for (uint32_t i = (uint32_t)lane; i < (uint32_t)Lay::HEADS / 16; i += 64)
+        for (uint32_t i = (uint32_t)lane; i < (uint32_t)Lay::GHEADS / 16; i += 64)
             reinterpret_cast<uint4 *>(heads)[i] = make_uint4(0, 0, 0, 0);
         team_sync<1>();
         // ---- pairs → heads, per referenced stream
@@ -791,7 +810,7 @@ __device__ __forceinline__ void decode_one(const DecodeArgs &a, uint8_t *smem, u
             uint32_t pidx = __builtin_amdgcn_readfirstlane(misc[D_PIDX + r]);
             uint32_t pos = __builtin_amdgcn_readfirstlane(misc[D_POS + r]);
             const uint32_t wstart = gwin * WPG * k;
-            const uint32_t wlen = WR * 64 * WPG * k;
+            const uint32_t wlen = GWR * 64 * WPG * k;
             const uint32_t hb = Lay::OFF_HEADS + 2u * hoff;
             while (pidx < np && pos - wstart < wlen) {
                 const uint32_t p0 = pidx + 8u * (uint32_t)lane;
@@ -861,7 +880,7 @@ __device__ __forceinline__ void decode_one(const DecodeArgs &a, uint8_t *smem, u
         team_sync<1>();
         PSY_PROF_MARK(9);
         // ---- per round: fill the planes, recombine, store
-        for (uint32_t rl = 0; rl < (uint32_t)WR; ++rl) {
+        for (uint32_t rl = 0; rl < GWR; ++rl) {
             const uint32_t g0 = gwin + rl * 64;
             if (g0 >= ngroups) break;
             // lane's 16 plane positions: heads[hoff + rl·64·WPG·k + fu ..)
@@ -930,7 +949,9 @@ __device__ __forceinline__ void decode_one(const DecodeArgs &a, uint8_t *smem, u
                 const uint64_t vb64 = wbytes - 16ull * g;
                 st16_any(dst + 16ull * g, o, vb64 >= 16 ? 16 : (int)vb64);
             }
-            team_sync<1>();  // planes are rewritten by the next round
+            // the planes' bytes are heads slots again: empty for the windows that follow (the
+            // gather's reads precede these writes in the wave's LDS order)
+            *reinterpret_cast<uint4 *>(planes + 16u * lane) = make_uint4(0, 0, 0, 0);
         }
         PSY_PROF_MARK(10);
     }
@@ -1204,7 +1225,7 @@ __global__ __launch_bounds__(64) void tdt_decode_ltile_kernel(DecodeArgs a) {
 // Blob ids: the look-back needs them in dispatch order (atomic ticket); slotted batches take
 // them from the plan's list (or, without one, the workgroup id).
 template <int LB, int WR = kDecWR>
-__global__ __launch_bounds__(64) void tdt_decode_kernel(DecodeArgs a) {
+__global__ __launch_bounds__(64, LB ? 6 : 8) void tdt_decode_kernel(DecodeArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t smem[DecLayoutT<WR>::BYTES];
     uint32_t msg;
     if constexpr (LB) {

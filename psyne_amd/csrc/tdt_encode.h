@@ -174,6 +174,7 @@ constexpr double kTieMargin = 1e-9;
 // per-wave slots (uint32, 8 per wave): 0,1 max(last run start+1); 2,3 chunk-start count;
 // 4 chunk bits of the wave's first group (combined slot layout)
 
+typedef uint32_t u32_a2 __attribute__((aligned(2)));  // a dword stored at a 2-byte aligned address
 __device__ __forceinline__ uint32_t popc(uint32_t x) { return (uint32_t)__builtin_popcount(x); }
 __device__ __forceinline__ uint32_t hibit(uint32_t x) { return 31u - (uint32_t)__builtin_clz(x); }
 __device__ __forceinline__ uint32_t lobit(uint32_t x) { return (uint32_t)__builtin_ctz(x); }
@@ -830,7 +831,7 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
                 const uint32_t fx = ((ed >> 16) ^ (pe >> 8)) & 0xffu;
                 m = (m & ~(1u << L0)) | ((fx ? 1u : 0u) << L0);
             }
-            if (g == 0) m |= 1u | (ns2 ? (1u << L0) : 0u);
+            if (g < 64u && g == 0u) m |= 1u | (ns2 ? (1u << L0) : 0u);  // (first test: uniform per round)
             return m & V;
         };
         // packed (stream 1 in the high half) round-relative last start + 1 of a start mask
@@ -914,6 +915,8 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
         // resident teams count in A2 (registers only; fewer live values across A1)
         uint32_t pc0 = 0, pc1 = 0;
         uint32_t fmx[2] = {0, 0};  // tile count pass: ~(first run start), max-reduced
+        // stream position of this lane's group in round 0 (round r adds r·64·Ls)
+        const uint32_t gL[2] = {(gw0 + (uint32_t)lane) * Ls[0], (gw0 + (uint32_t)lane) * Ls[1]};
         {
             uint32_t edc = edc0;
             for_rounds([&](uint32_t r, uint4 &d, uint32_t &cm, auto res) __attribute__((always_inline)) {
@@ -928,7 +931,7 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
                 cm = m;
                 if constexpr (decltype(res)::value) d = make_uint4(T[0], T[1], T[2], T[3]);
                 const uint32_t m0 = m & lowL0;
-                if (m0) wmax[0] = umax(wmax[0], g * Ls[0] + hibit(m0) + 1u);
+                if (m0) wmax[0] = umax(wmax[0], gL[0] + r * 64u * Ls[0] + hibit(m0) + 1u);
                 if constexpr (!decltype(res)::value) pc0 += popc(m0);
                 if constexpr (TL == 2) {
                     if (m0) fmx[0] = umax(fmx[0], ~(g * Ls[0] + lobit(m0)));
@@ -938,7 +941,7 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
                 zacc |= (b0 - zk1[0]) & ~b0 & zk8[0];
                 if (ns2) {
                     const uint32_t m1 = m >> L0;
-                    if (m1) wmax[1] = umax(wmax[1], g * Ls[1] + hibit(m1) + 1u);
+                    if (m1) wmax[1] = umax(wmax[1], gL[1] + r * 64u * Ls[1] + hibit(m1) + 1u);
                     if constexpr (!decltype(res)::value) pc1 += popc(m1);
                     if constexpr (TL == 2) {
                         if (m1) fmx[1] = umax(fmx[1], ~(g * Ls[1] + lobit(m1)));
@@ -1247,7 +1250,9 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
         // last-entry read, the pending entry, loop set-up) is paid once per pair of rounds.
         constexpr bool E6 = RES && WS <= 4;
         const uint32_t eb6 = wst + 16u;
-        const uint32_t eoff6 = 2u * (1u + 128u * L0);  // stream 1's u16 region (bytes)
+        // stream 1's u16 region (bytes; a multiple of 4 like eb6, so that every region's even
+        // entries are dword-aligned for the flush)
+        const uint32_t eoff6 = 2u * (2u + 128u * L0);
         uint32_t s6[2] = {0, 0};  // entries of the current batch, per stream
         uint32_t pend6[2] = {0, 0};
 #pragma unroll
@@ -1272,8 +1277,10 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
             const uint32_t pinc = wave_incl_scan<OpAdd>(pc);
             const uint32_t pexc = pinc - pc;
             const uint32_t Stot = rdlane(pinc, 63);
-            const uint32_t D0 = eb6 + 2u * (1u + s6[0] + (pexc & 0xffffu)) - jl;
-            const uint32_t D1 = eb6 + eoff6 + 2u * (1u + s6[1] + (pexc >> 16)) - jl;
+            // entry 0 of a region holds the pending chunk (when there is one); the batch's own
+            // entries follow it
+            const uint32_t D0 = eb6 + 2u * ((hp[0] ? 1u : 0u) + s6[0] + (pexc & 0xffffu)) - jl;
+            const uint32_t D1 = eb6 + eoff6 + 2u * ((hp[1] ? 1u : 0u) + s6[1] + (pexc >> 16)) - jl;
             uint32_t D = L0 == 0 ? D1 : D0;
             // entries of slots q + 4t, two per dword: E[q][0] = slots q, q+4; E[q][1] = q+8, q+12
             uint32_t E[4][2];
@@ -1306,30 +1313,41 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
 #pragma unroll
             for (int c = 0; c < 2; ++c) {
                 if (c == 1 && !ns2) break;
-                const uint32_t f0 = hp[c] ? 0u : 1u;
                 const uint32_t nent = s6[c] + (hp[c] ? 1u : 0u);
-                const uint32_t K = nent ? nent - 1u : 0u;
+                const uint32_t K = nent ? nent - 1u : 0u;  // pair k = entries k, k + 1
                 const uint32_t eb = eb6 + (c ? eoff6 : 0u);
                 uint8_t *const Dp = dst + sdata[c] + 2ull * pi5[c];
                 auto pair_at = [&](uint32_t k) __attribute__((always_inline)) -> uint32_t {
-                    const uint32_t e0 = *reinterpret_cast<const uint16_t *>(smem + eb + 2u * (f0 + k));
-                    const uint32_t e1 = *reinterpret_cast<const uint16_t *>(smem + eb + 2u * (f0 + k + 1u));
+                    const uint32_t e0 = *reinterpret_cast<const uint16_t *>(smem + eb + 2u * k);
+                    const uint32_t e1 = *reinterpret_cast<const uint16_t *>(smem + eb + 2u * k + 2u);
                     return perm(e0, e1 - e0, 0x0c0c0500u);  // count = (e1 - e0) mod 256, value
                 };
+                // pairs k, k + 1 (k even) from entries k..k+2: one aligned dword and one u16 read,
+                // both counts by one packed u16 subtract, one v_perm into (c0, v0, c1, v1)
+                auto pairs2_at = [&](uint32_t k) __attribute__((always_inline)) -> uint32_t {
+                    const uint32_t E01 = *reinterpret_cast<const uint32_t *>(smem + eb + 2u * k);
+                    const uint32_t e2 = *reinterpret_cast<const uint16_t *>(smem + eb + 2u * k + 4u);
+                    const uint32_t E12 = __builtin_amdgcn_alignbyte(e2, E01, 2);
+                    uint32_t d;
+                    asm("v_pk_sub_u16 %0, %1, %2" : "=v"(d) : "v"(E12), "v"(E01));
+                    return perm(E01, d, 0x07020500u);
+                };
                 if (((uintptr_t)Dp & 1) == 0) {
+                    // lane l stores pairs k0 + 2l, k0 + 2l + 1 with one (2-byte aligned) dword store
                     uint32_t k0 = 0;
+                    for (; k0 + 256u <= K; k0 += 256u) {
+                        const uint32_t k = k0 + 2u * (uint32_t)lane;
+                        const uint32_t pa = pairs2_at(k), pb = pairs2_at(k + 128u);
+                        *reinterpret_cast<u32_a2 *>(Dp + 2u * k) = pa;
+                        *reinterpret_cast<u32_a2 *>(Dp + 2u * k + 256u) = pb;
+                    }
                     for (; k0 + 128u <= K; k0 += 128u) {
-                        const uint32_t k = k0 + (uint32_t)lane;
-                        const uint32_t pa = pair_at(k), pb = pair_at(k + 64u);
-                        *reinterpret_cast<uint16_t *>(Dp + 2u * k) = (uint16_t)pa;
-                        *reinterpret_cast<uint16_t *>(Dp + 2u * k + 128u) = (uint16_t)pb;
+                        const uint32_t k = k0 + 2u * (uint32_t)lane;
+                        *reinterpret_cast<u32_a2 *>(Dp + 2u * k) = pairs2_at(k);
                     }
-                    for (; k0 + 64u <= K; k0 += 64u) {
-                        const uint32_t k = k0 + (uint32_t)lane;
-                        *reinterpret_cast<uint16_t *>(Dp + 2u * k) = (uint16_t)pair_at(k);
-                    }
-                    const uint32_t k = k0 + (uint32_t)lane;
-                    if (k < K) *reinterpret_cast<uint16_t *>(Dp + 2u * k) = (uint16_t)pair_at(k);
+                    const uint32_t k = k0 + 2u * (uint32_t)lane;
+                    if (k + 1u < K) *reinterpret_cast<u32_a2 *>(Dp + 2u * k) = pairs2_at(k);
+                    else if (k < K) *reinterpret_cast<uint16_t *>(Dp + 2u * k) = (uint16_t)pair_at(k);
                 } else {
                     for (uint32_t k0 = 0; k0 < K; k0 += 64) {
                         const uint32_t k = k0 + (uint32_t)lane;
@@ -1342,7 +1360,7 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
                 }
                 pi5[c] += K;
                 if (nent) {
-                    const uint32_t el = __builtin_amdgcn_readfirstlane(*reinterpret_cast<const uint16_t *>(smem + eb + 2u * s6[c]));
+                    const uint32_t el = __builtin_amdgcn_readfirstlane(*reinterpret_cast<const uint16_t *>(smem + eb + 2u * K));
                     if (last) {  // the final chunk runs to the end of the stream
                         if (lane == 0) {
                             Dp[2u * K] = (uint8_t)(slen[c] - el);
