@@ -27,6 +27,13 @@ __device__ unsigned long long psy_prof[32];
         if (lane_id() == 0) atomicAdd(&psy_prof[(i)], psy_t_ - psy_pt_);    \
         psy_pt_ = psy_t_;                                                   \
     } while (0)
+#elif defined(PSY_X_STOP)
+// diagnostic attribution builds: the encode kernel returns at phase mark PSY_X_STOP
+#define PSY_PROF_BEGIN() ((void)0)
+#define PSY_PROF_MARK(i)                        \
+    do {                                        \
+        if ((i) == PSY_X_STOP) return;          \
+    } while (0)
 #elif defined(PSY_ASM_MARKS)
 #define PSY_PROF_BEGIN() ((void)0)
 #define PSY_PROF_MARK(i) asm volatile(";@@MARK " #i ::)
