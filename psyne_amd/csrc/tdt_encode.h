@@ -826,10 +826,17 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
             return v;
         };
         // run-start mask of the 16 slots (bit j: slot j differs from the stream byte before)
-        auto run_mask = [&](const uint32_t (&T)[4], uint32_t ed, uint32_t edc, uint32_t g,
+        // P0 = the byte before each slot of T[0]: byte t = slot 4t - 1 of the group, byte 0 the
+        // previous group's last stream-0 byte.  When stream 1 begins at a dword boundary
+        // (L0 % 4 == 0: word size <= 4), its first slot L0 = 4·t0 takes the previous group's last
+        // stream-1 byte (edges byte 1) instead, folded into the selector once per message.
+        constexpr bool kFold = WS <= 4;  // L0 = (16 / WS)·k0 is then a multiple of 4
+        const uint32_t p0sel = kFold && ns2 ? (0x06050400u & ~(0xffu << (2u * L0))) | (0x01u << (2u * L0)) : 0x06050400u;
+        // first: this round holds the message's group 0 (uniform)
+        auto run_mask = [&](const uint32_t (&T)[4], uint32_t ed, uint32_t edc, bool first,
                             uint32_t V) __attribute__((always_inline)) -> uint32_t {
             const uint32_t pe = wave_shr1(ed, edc);  // previous group's edges
-            const uint32_t P0 = perm(T[3], pe, 0x06050400u);
+            const uint32_t P0 = perm(T[3], pe, p0sel);
             const uint32_t X[4] = {T[0] ^ P0, T[1] ^ T[0], T[2] ^ T[1], T[3] ^ T[2]};
             uint32_t m = 0;
 #pragma unroll
@@ -839,11 +846,13 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
             }
             m = (m | (m >> 4)) & 0x00ff00ffu;
             m = (m | (m >> 8)) & 0xffffu;
-            if (ns2) {
-                const uint32_t fx = ((ed >> 16) ^ (pe >> 8)) & 0xffu;
-                m = (m & ~(1u << L0)) | ((fx ? 1u : 0u) << L0);
+            if constexpr (!kFold) {
+                if (ns2) {
+                    const uint32_t fx = ((ed >> 16) ^ (pe >> 8)) & 0xffu;
+                    m = (m & ~(1u << L0)) | ((fx ? 1u : 0u) << L0);
+                }
             }
-            if (g < 64u && g == 0u) m |= 1u | (ns2 ? (1u << L0) : 0u);  // (first test: uniform per round)
+            if (first && lane == 0) m |= 1u | (ns2 ? (1u << L0) : 0u);
             return m & V;
         };
         // packed (stream 1 in the high half) round-relative last start + 1 of a start mask
@@ -914,6 +923,8 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
         // has-zero-byte (B = 8) or has-zero-nibble (B = 4) test on it, on the scalar unit
         // (tests/test_cap_exclusion.py checks the rule against adversarial run lengths).
         uint32_t wmax[2] = {0, 0};
+        uint32_t lr[2] = {0, 0};        // resident: last round with a run start, per stream
+        uint64_t lb[2] = {0ull, 0ull};  // and that round's ballot of lanes with one
         uint64_t zk1[2], zk8[2];
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
@@ -934,37 +945,70 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
             for_rounds([&](uint32_t r, uint4 &d, uint32_t &cm, auto res) __attribute__((always_inline)) {
                 PSY_ASM_ROUND(A1);
                 const uint32_t g = gw0 + r * 64 + lane;
+                const uint32_t ed = edges(d);
                 uint32_t T[4];
                 tmat(d, T);
-                const uint32_t ed = edges(d);
                 const uint32_t V = full_round(r) ? 0xffffu : vmask(vbytes(g));
-                const uint32_t m = run_mask(T, ed, edc, g, V);
+                const uint32_t m = run_mask(T, ed, edc, r == 0u && gw0 == 0u, V);
                 edc = rdlane(ed, 63);
                 cm = m;
                 if constexpr (decltype(res)::value) d = make_uint4(T[0], T[1], T[2], T[3]);
+                constexpr bool SW = decltype(res)::value && TL != 2;  // scalar last-start tracking
                 const uint32_t m0 = m & lowL0;
-                if (m0) wmax[0] = umax(wmax[0], gL[0] + r * 64u * Ls[0] + hibit(m0) + 1u);
+                const uint64_t r0 = (uint64_t)__ballot(m0 != 0u);
+                if constexpr (SW) {
+                    if (r0) {
+                        lr[0] = r;
+                        lb[0] = r0;
+                    }
+                } else {
+                    if (m0) wmax[0] = umax(wmax[0], gL[0] + r * 64u * Ls[0] + hibit(m0) + 1u);
+                }
                 if constexpr (!decltype(res)::value) pc0 += popc(m0);
                 if constexpr (TL == 2) {
                     if (m0) fmx[0] = umax(fmx[0], ~(g * Ls[0] + lobit(m0)));
                 }
                 const uint64_t pastm = full_round(r) ? 0ull : (uint64_t)__ballot(g >= ngroups);
-                const uint64_t b0 = (uint64_t)__ballot(m0 != 0u) | pastm;
+                const uint64_t b0 = r0 | pastm;
                 zacc |= (b0 - zk1[0]) & ~b0 & zk8[0];
                 if (ns2) {
                     const uint32_t m1 = m >> L0;
-                    if (m1) wmax[1] = umax(wmax[1], gL[1] + r * 64u * Ls[1] + hibit(m1) + 1u);
+                    const uint64_t r1 = (uint64_t)__ballot(m1 != 0u);
+                    if constexpr (SW) {
+                        if (r1) {
+                            lr[1] = r;
+                            lb[1] = r1;
+                        }
+                    } else {
+                        if (m1) wmax[1] = umax(wmax[1], gL[1] + r * 64u * Ls[1] + hibit(m1) + 1u);
+                    }
                     if constexpr (!decltype(res)::value) pc1 += popc(m1);
                     if constexpr (TL == 2) {
                         if (m1) fmx[1] = umax(fmx[1], ~(g * Ls[1] + lobit(m1)));
                     }
-                    const uint64_t b1 = (uint64_t)__ballot(m1 != 0u) | pastm;
+                    const uint64_t b1 = r1 | pastm;
                     zacc |= (b1 - zk1[1]) & ~b1 & zk8[1];
                 }
             });
         }
-        wmax[0] = wave_reduce<OpMax>(wmax[0]);
-        wmax[1] = wave_reduce<OpMax>(wmax[1]);
+        if constexpr (RES && TL != 2) {
+            // the wave's last run start per stream: in the last round with a start, its highest
+            // lane with one (all scalar but one readlane per stream)
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                if (lb[c] == 0ull) continue;
+                const uint32_t l = 63u - (uint32_t)__builtin_clzll(lb[c]);
+                uint32_t mv = 0;
+#pragma unroll
+                for (int r = 0; r < GR; ++r)
+                    if ((uint32_t)r == lr[c]) mv = rdlane(cres[r], (int)l);
+                const uint32_t mc = c ? mv >> L0 : mv & lowL0;
+                wmax[c] = (gw0 + lr[c] * 64u + l) * Ls[c] + hibit(mc) + 1u;
+            }
+        } else {
+            wmax[0] = wave_reduce<OpMax>(wmax[0]);
+            wmax[1] = wave_reduce<OpMax>(wmax[1]);
+        }
         if constexpr (TL == 2) {
             fmx[0] = wave_reduce<OpMax>(fmx[0]);
             fmx[1] = wave_reduce<OpMax>(fmx[1]);
@@ -1018,7 +1062,7 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
                     uint32_t T[4];
                     tmat(d, T);
                     const uint32_t ed = edges(d);
-                    m = run_mask(T, ed, edc, g, V);
+                    m = run_mask(T, ed, edc, r == 0u && gw0 == 0u, V);
                     edc = rdlane(ed, 63);
                 }
                 const uint32_t C = clean ? m : chunk_round(r, m, rcarry, g, V);
@@ -1426,7 +1470,7 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
                 tmat(d, T);
                 Tw = make_uint4(T[0], T[1], T[2], T[3]);
                 const uint32_t ed = edges(d);
-                const uint32_t m = run_mask(T, ed, edc, g, V);
+                const uint32_t m = run_mask(T, ed, edc, r == 0u && gw0 == 0u, V);
                 edc = rdlane(ed, 63);
                 return clean ? m : chunk_round(r, m, rcarry, g, V);
             };
