@@ -964,7 +964,7 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
                 } else {
                     if (m0) wmax[0] = umax(wmax[0], gL[0] + r * 64u * Ls[0] + hibit(m0) + 1u);
                 }
-                if constexpr (!decltype(res)::value) pc0 += popc(m0);
+                pc0 += popc(m0);
                 if constexpr (TL == 2) {
                     if (m0) fmx[0] = umax(fmx[0], ~(g * Ls[0] + lobit(m0)));
                 }
@@ -973,7 +973,7 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
                 zacc |= (b0 - zk1[0]) & ~b0 & zk8[0];
                 if (ns2) {
                     const uint32_t m1 = m >> L0;
-                    const uint64_t r1 = (uint64_t)__ballot(m1 != 0u);
+                    const uint64_t r1 = (uint64_t)__ballot(m > lowL0);  // m1 != 0 (m < 2^16)
                     if constexpr (SW) {
                         if (r1) {
                             lr[1] = r;
@@ -982,7 +982,7 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
                     } else {
                         if (m1) wmax[1] = umax(wmax[1], gL[1] + r * 64u * Ls[1] + hibit(m1) + 1u);
                     }
-                    if constexpr (!decltype(res)::value) pc1 += popc(m1);
+                    pc1 += popc(m1);
                     if constexpr (TL == 2) {
                         if (m1) fmx[1] = umax(fmx[1], ~(g * Ls[1] + lobit(m1)));
                     }
@@ -1013,9 +1013,15 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
             fmx[0] = wave_reduce<OpMax>(fmx[0]);
             fmx[1] = wave_reduce<OpMax>(fmx[1]);
         }
+        // run-start counts: the chunk-start counts whenever the 255-cap is ruled out (A2 then
+        // never runs and its barrier is saved)
+        pc0 = wave_reduce<OpAdd>(pc0);
+        pc1 = ns2 ? wave_reduce<OpAdd>(pc1) : 0u;
         if (lane == 0) {
             slots[wv * 8 + 0] = wmax[0];
             slots[wv * 8 + 1] = wmax[1];
+            slots[wv * 8 + 2] = pc0;
+            slots[wv * 8 + 3] = pc1;
             slots[wv * 8 + 5] = zacc != 0ull ? 1u : 0u;
             if constexpr (TL == 2) {
                 slots[wv * 8 + 6] = fmx[0];
@@ -1047,7 +1053,7 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
         PSY_PROF_MARK(3);
 
         // ---------------------------------------------------------- pass A2: chunk starts
-        if (RES || !clean) {
+        if (!clean) {
             pc0 = pc1 = 0;
             uint32_t rcarry[2] = {rin[0], rin[1]};
             uint32_t edc = edc0;
@@ -1065,19 +1071,19 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
                     m = run_mask(T, ed, edc, r == 0u && gw0 == 0u, V);
                     edc = rdlane(ed, 63);
                 }
-                const uint32_t C = clean ? m : chunk_round(r, m, rcarry, g, V);
+                const uint32_t C = chunk_round(r, m, rcarry, g, V);
                 cm = C;
                 pc0 += popc(C & lowL0);
                 pc1 += popc(C >> L0);
             });
+            pc0 = wave_reduce<OpAdd>(pc0);
+            pc1 = ns2 ? wave_reduce<OpAdd>(pc1) : 0u;
+            if (lane == 0) {  // (slots 2, 3 are first read after the barrier below)
+                slots[wv * 8 + 2] = pc0;
+                slots[wv * 8 + 3] = pc1;
+            }
+            team_sync<W>();
         }
-        pc0 = wave_reduce<OpAdd>(pc0);
-        pc1 = ns2 ? wave_reduce<OpAdd>(pc1) : 0u;
-        if (lane == 0) {
-            slots[wv * 8 + 2] = pc0;
-            slots[wv * 8 + 3] = pc1;
-        }
-        team_sync<W>();
         PSY_PROF_MARK(4);
         uint32_t pin[2] = {0, 0}, ptot[2] = {0, 0};
 #pragma unroll
