@@ -465,6 +465,28 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
                 }
             }
         };
+        const double *ltab = W == 1 ? c_log2_tab : reinterpret_cast<const double *>(smem + Lay::OFF_LOG2);
+        const double *ltab2 = W == 1 ? c_log2_tab2 : ltab + 128;
+        const double total = (double)wc;
+        // Counts repeat: the terms of counts 1..64 are computed once per message (exactly the
+        // operations below, so the same bits) and looked up; larger counts are computed.  Lane i
+        // holds count i + 1's terms (one-wave teams: in registers, looked up by ds_bpermute).
+        double *ctab = reinterpret_cast<double *>(smem + Lay::OFF_CTAB);
+        // (computed before the histogram: the barrier after it publishes the table)
+        double c_np = 0.0, c_L = 0.0;
+        if (TL != 1 && tid < 64) {
+            double prob;
+            {
+#pragma clang fp contract(off)
+                prob = (double)(uint32_t)(tid + 1) / total;
+                c_L = psy_log2_glibc(prob, ltab, ltab2);
+            }
+            c_np = -prob;
+            if constexpr (W > 1) {
+                ctab[2 * tid] = c_np;
+                ctab[2 * tid + 1] = c_L;
+            }
+        }
         if constexpr (TL != 4)
         for_rounds([&](uint32_t r, uint4 &d, uint32_t &, auto) __attribute__((always_inline)) {
             PSY_ASM_ROUND(H);
@@ -500,28 +522,6 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
         // needs no select: fma(0, 0, e) == e for the non-negative running sum); then in every
         // wave one lane per position runs the exact fma chain in bin order.
         double *terms = reinterpret_cast<double *>(smem + Lay::OFF_TERMS);
-        const double *ltab = W == 1 ? c_log2_tab : reinterpret_cast<const double *>(smem + Lay::OFF_LOG2);
-        const double *ltab2 = W == 1 ? c_log2_tab2 : ltab + 128;
-        const double total = (double)wc;
-        // Counts repeat: the terms of counts 1..64 are computed once per message (exactly the
-        // operations below, so the same bits) and looked up; larger counts are computed.  Lane i
-        // holds count i + 1's terms (one-wave teams: in registers, looked up by ds_bpermute).
-        double *ctab = reinterpret_cast<double *>(smem + Lay::OFF_CTAB);
-        double c_np = 0.0, c_L = 0.0;
-        if (tid < 64) {
-            double prob;
-            {
-#pragma clang fp contract(off)
-                prob = (double)(uint32_t)(tid + 1) / total;
-                c_L = psy_log2_glibc(prob, ltab, ltab2);
-            }
-            c_np = -prob;
-            if constexpr (W > 1) {
-                ctab[2 * tid] = c_np;
-                ctab[2 * tid + 1] = c_L;
-            }
-        }
-        team_sync<W>();
         // (-prob, log2 prob) of a bin with count c
         auto shfl_f64 = [&](double x, uint32_t src) __attribute__((always_inline)) -> double {
             const uint64_t u = __builtin_bit_cast(uint64_t, x);
