@@ -385,14 +385,19 @@ __device__ __forceinline__ void decode_fast(const FastHdr &H, uint8_t *smem, con
             uint8_t *const planes = smem + pl_base + rl * pl_step;
             // lanes 8-15 of every 16 read their second half first: with 32-byte lane rows the
             // two ds_read_b128 are then bank-conflict-free (MI355X_MICROARCH.md §LDS groups)
+#ifndef PSY_DEC_NOSWAP
             const bool sw = (lane & 8u) != 0u;
             const uint4 ha = *reinterpret_cast<const uint4 *>(smem + hoffb + (sw ? 16u : 0u));
             const uint4 hb = *reinterpret_cast<const uint4 *>(smem + hoffb + (sw ? 0u : 16u));
             const uint4 h0 = sw ? hb : ha, h1 = sw ? ha : hb;
+#else
+            const uint4 h0 = *reinterpret_cast<const uint4 *>(smem + hoffb);
+            const uint4 h1 = *reinterpret_cast<const uint4 *>(smem + hoffb + 16u);
+#endif
             uint32_t x[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
             uint32_t m = pk_max_u16(pk_max_u16(pk_max_u16(x[0], x[1]), pk_max_u16(x[2], x[3])),
                                     pk_max_u16(pk_max_u16(x[4], x[5]), pk_max_u16(x[6], x[7])));
-            m = pk_max_u16(m, m >> 16) & 0xffffu;
+            m = pk_max_self_lo(m) >> 16;
             // a current head exists in the lane iff the max key carries this window's gen and a tag
             const bool hv = (m >> 13) == gen && ((m >> 8) & 31u) != 0u;
             const uint32_t lk = hv ? ((lane + 1u) << 8) | (m & 0xffu) : 0u;
@@ -402,9 +407,9 @@ __device__ __forceinline__ void decode_fast(const FastHdr &H, uint8_t *smem, con
             const uint32_t seed = (gen << 13) | seedv;
             x[0] = pk_max_u16(x[0], seed);
 #pragma unroll
-            for (int q = 0; q < 8; ++q) x[q] = pk_max_u16(x[q], x[q] << 16);
+            for (int q = 0; q < 8; ++q) x[q] = pk_max_self_lo(x[q]);
 #pragma unroll
-            for (int q = 1; q < 8; ++q) x[q] = pk_max_u16(x[q], perm(x[q - 1], x[q - 1], 0x03020302u));
+            for (int q = 1; q < 8; ++q) x[q] = pk_max_bcast_hi(x[q], x[q - 1]);
             uint32_t bw[4] = {perm(x[1], x[0], 0x06040200u), perm(x[3], x[2], 0x06040200u),
                               perm(x[5], x[4], 0x06040200u), perm(x[7], x[6], 0x06040200u)};
             // a stream that ran out of pairs leaves zeros (recombine :626-631)
@@ -891,7 +896,7 @@ __device__ __forceinline__ void decode_one(const DecodeArgs &a, uint8_t *smem, u
             // last head key of the lane (tags order the keys by position)
             uint32_t m = pk_max_u16(pk_max_u16(pk_max_u16(x[0], x[1]), pk_max_u16(x[2], x[3])),
                                     pk_max_u16(pk_max_u16(x[4], x[5]), pk_max_u16(x[6], x[7])));
-            m = pk_max_u16(m, m >> 16) & 0xffffu;
+            m = pk_max_self_lo(m) >> 16;
             const uint32_t lk = m ? (((uint32_t)lane + 1u) << 8) | (m & 0xffu) : 0u;
             const uint32_t ex = wave_shr1(wave_incl_scan<OpMax>(lk), 0u);
             uint32_t seed;
@@ -900,9 +905,9 @@ __device__ __forceinline__ void decode_one(const DecodeArgs &a, uint8_t *smem, u
             x[0] = pk_max_u16(x[0], seed);
             // in-lane prefix max: within each dword, then across dwords
 #pragma unroll
-            for (int q = 0; q < 8; ++q) x[q] = pk_max_u16(x[q], x[q] << 16);
+            for (int q = 0; q < 8; ++q) x[q] = pk_max_self_lo(x[q]);
 #pragma unroll
-            for (int q = 1; q < 8; ++q) x[q] = pk_max_u16(x[q], perm(x[q - 1], x[q - 1], 0x03020302u));
+            for (int q = 1; q < 8; ++q) x[q] = pk_max_bcast_hi(x[q], x[q - 1]);
             uint4 bytes = make_uint4(perm(x[1], x[0], 0x06040200u), perm(x[3], x[2], 0x06040200u),
                                      perm(x[5], x[4], 0x06040200u), perm(x[7], x[6], 0x06040200u));
             // a stream that ran out of pairs leaves zeros (recombine :626-631)

@@ -115,6 +115,18 @@ __device__ __forceinline__ uint32_t pk_max_u16(uint32_t a, uint32_t b) {
     return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(psy_u16x2, a),
                                                                   __builtin_bit_cast(psy_u16x2, b)));
 }
+// (lo, max(hi, lo)) and (max(a.lo, b.hi), max(a.hi, b.hi)): one v_pk_max_u16 each, the half
+// broadcast folded into the instruction's op_sel (no shift / v_perm in front of it).
+__device__ __forceinline__ uint32_t pk_max_self_lo(uint32_t a) {
+    uint32_t r;
+    asm("v_pk_max_u16 %0, %1, %1 op_sel:[0,0] op_sel_hi:[1,0]" : "=v"(r) : "v"(a));
+    return r;
+}
+__device__ __forceinline__ uint32_t pk_max_bcast_hi(uint32_t a, uint32_t b) {
+    uint32_t r;
+    asm("v_pk_max_u16 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,1]" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
 // Two independent u16 adds per dword (v_pk_add_u16, no carry between the halves).
 __device__ __forceinline__ uint32_t pk_add_u16(uint32_t a, uint32_t b) {
     return __builtin_bit_cast(uint32_t, __builtin_bit_cast(psy_u16x2, a) + __builtin_bit_cast(psy_u16x2, b));
