@@ -101,7 +101,8 @@ __device__ __forceinline__ uint4 ld16_span(const uint8_t *p, int valid, const ui
     if (valid >= 16 && a0 + 20 <= (uintptr_t)lim) {
         const uint32_t *q = reinterpret_cast<const uint32_t *>(a0);
         const uint32_t sh = (uint32_t)(a & 3);
-        const uint32_t w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3], w4 = q[4];
+        const uint32_t w0 = gload<uint32_t>(q), w1 = gload<uint32_t>(q + 1), w2 = gload<uint32_t>(q + 2),
+                       w3 = gload<uint32_t>(q + 3), w4 = gload<uint32_t>(q + 4);
         if (sh == 0) return make_uint4(w0, w1, w2, w3);
         return make_uint4(__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
                           __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh));

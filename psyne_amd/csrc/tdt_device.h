@@ -380,6 +380,13 @@ __device__ __forceinline__ uint64_t lookback_excl_wave(uint64_t *st, uint32_t i,
 }
 
 // ---------------------------------------------------------------------------------------
+// Loads through the global address space (kernel-argument pointers reach the device code as
+// generic pointers; flat loads would also count in lgkmcnt and wait behind LDS traffic).
+template <class T>
+__device__ __forceinline__ T gload(const void *p) {
+    return *(const __attribute__((address_space(1))) T *)(p);
+}
+
 // Byte-exact accesses.
 __device__ __forceinline__ uint32_t ld_u8(const uint8_t *p) { return *p; }
 
