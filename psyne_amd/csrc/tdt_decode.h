@@ -58,7 +58,7 @@ struct DecodeArgs {
 constexpr int kMaxRef = 16;  // referenced streams <= word_size <= 16
 constexpr uint32_t kDecTileGroups = 2048;  // large blobs: 32 KiB of output per tile
 #ifndef PSY_DEC_WR
-#define PSY_DEC_WR 2
+#define PSY_DEC_WR 3
 #endif
 constexpr int kDecWR = PSY_DEC_WR;  // rounds per window
 constexpr int kHdrCache = 256;
@@ -247,7 +247,10 @@ __device__ __forceinline__ void decode_fast(const FastHdr &H, uint8_t *smem, con
     const bool f1 = lane * 16u >= 64u * seg[0];
     const uint32_t fu = f1 ? lane * 16u - 64u * seg[0] : lane * 16u;
     const uint32_t fseg = f1 ? seg[1] : seg[0];
-    const uint32_t f_lb = f1 ? 4u * seg[0] : 0u;  // first lane of this lane's stream plane
+    // scan tags: (lane + 1) << 8, + 64 << 8 on stream-1 lanes; lthr: the lowest tag of this
+    // lane's stream
+    const uint32_t ltag = (lane + 1u + (f1 ? 64u : 0u)) << 8;
+    const uint32_t lthr = f1 ? (65u << 8) : (1u << 8);
     const uint32_t fh = (f1 ? hbase[1] : hbase[0]) + 2u * fu;
     const uint32_t last_lane0 = 4u * seg[0] - 1u;  // lane holding stream 0's last plane byte
     // recombine: S dword d (S = the group's seg[0] stream-0 bytes, then its seg[1] stream-1
@@ -399,12 +402,14 @@ __device__ __forceinline__ void decode_fast(const FastHdr &H, uint8_t *smem, con
             uint32_t m = pk_max_u16(pk_max_u16(pk_max_u16(x[0], x[1]), pk_max_u16(x[2], x[3])),
                                     pk_max_u16(pk_max_u16(x[4], x[5]), pk_max_u16(x[6], x[7])));
             m = pk_max_self_lo(m) >> 16;
-            // a current head exists in the lane iff the max key carries this window's gen and a tag
-            const bool hv = (m >> 13) == gen && ((m >> 8) & 31u) != 0u;
-            const uint32_t lk = hv ? ((lane + 1u) << 8) | (m & 0xffu) : 0u;
+            // a current head exists in the lane iff the max key carries this window's gen and a
+            // tag (older gens only hold smaller keys); the lane's tag orders the scan, stream-1
+            // lanes tagged above every stream-0 lane, so one compare tells a head earlier in the
+            // lane's own stream plane from the carry
+            const uint32_t lk = m >= ((gen << 13) | 0x100u) ? perm(ltag, m, 0x07060500u) : 0u;
             const uint32_t ex = wave_shr1(wave_incl_scan<OpMax>(lk), 0u);
             const uint32_t carry = f1 ? cv[1] : cv[0];
-            const uint32_t seedv = (ex && (ex >> 8) - 1u >= f_lb) ? (ex & 0xffu) : carry;
+            const uint32_t seedv = ex >= lthr ? (ex & 0xffu) : carry;
             const uint32_t seed = (gen << 13) | seedv;
             x[0] = pk_max_u16(x[0], seed);
 #pragma unroll
