@@ -295,10 +295,11 @@ __device__ __forceinline__ void decode_fast(const FastHdr &H, uint8_t *smem, con
             const uint32_t c0 = w & 0xffu, c1 = (w >> 16) & 0xffu;
             // key = (pos mod 16 + 1) << 8 | value; value bytes 1 and 3 of the dword
             const uint32_t k0 = ((((run & 15u) + 1u) << 8) | ((w >> 8) & 0xffu));
-            st[r][2 * j] = (c0 != 0u && (uint32_t)(2 * j) < nv) ? run : ~0u;
+            // (pairs past the stream's end were loaded as zero bytes: count 0, no extra test)
+            st[r][2 * j] = c0 != 0u ? run : ~0u;
             run += c0;
             const uint32_t k1 = ((((run & 15u) + 1u) << 8) | (w >> 24));
-            st[r][2 * j + 1] = (c1 != 0u && (uint32_t)(2 * j + 1) < nv) ? run : ~0u;
+            st[r][2 * j + 1] = c1 != 0u ? run : ~0u;
             run += c1;
             kp[r][j] = k0 | (k1 << 16);
         }

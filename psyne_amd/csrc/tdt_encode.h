@@ -448,14 +448,17 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
             const uint32_t dw[4] = {d.x, d.y, d.z, d.w};
 #pragma unroll
             for (int i = 0; i < 16; i += 2) {
-                const uint32_t P = perm(0u, dw[i >> 2], (i & 2) ? 0x0c030c02u : 0x0c010c00u);
+                // bytes (0, 2) of a dword with one v_and, bytes (1, 3) with v_lshrrev + v_and
+                // (2-cycle ops, where a v_perm costs 4)
+                const int w = i >> 2, o = (i >> 1) & 1;
+                const uint32_t P = (o ? dw[w] >> 8 : dw[w]) & 0x00ff00ffu;
                 uint32_t A;
                 asm("v_pk_mad_u16 %0, %1, %2, %3" : "=v"(A) : "v"(P), "s"(kMul2), "v"(coff2));
                 asm("v_pk_min_u16 %0, %1, %2" : "=v"(A) : "v"(A), "v"(zoff2));
                 const uint32_t ad2[2] = {A & 0xffffu, A >> 16};
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
-                    const int b = i + h;
+                    const int b = 4 * w + o + 2 * h;
 #ifndef PSY_X_NOHIST
                     if (full || (uint32_t)b < vb)
 #else
