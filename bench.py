@@ -62,6 +62,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = all usable host cores")
     ap.add_argument("--cpu-kind", choices=["reference", "port"], default="reference")
     ap.add_argument("--host-inclusive", action="store_true", help="also time pinned H2D+kernel+D2H")
+    ap.add_argument("--compacted-steps", type=int, default=3,
+                    help="timed steps of the compacted (look-back) API leg after the headline (0 = skip)")
     ap.add_argument("--seed", type=int, default=None)
     ap.add_argument("--workload", choices=["c2", "c3", "c4"], default="c3",
                     help="c3 (default, the BASELINE metric): 262,144 x 64 KiB gradient; c2: 1 Mi x 1 KiB "
@@ -386,6 +388,42 @@ def main():
     ms_per_step = job_elapsed / a.steps * 1e3
     value = job_payload * a.steps / job_elapsed / 2**30
 
+    # Compacted API leg (tdt_encode_batch / tdt_decode_batch: blobs and decoded messages packed
+    # in message order, offsets by the kernels' decoupled look-back — the north_star's
+    # variable-length output compaction), on the same batch after the timed loop; reported
+    # beside the headline, never as `value`.  Reuses the slotted buffers.
+    compacted = None
+    if a.compacted_steps > 0:
+        coff = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        cdoff = torch.empty(n + 1, dtype=torch.int64, device=dev)
+
+        def cstep(ev=None):
+            if ev:
+                ev[0].record(stream)
+            check(lib.tdt_encode_batch(h, P(data), P(off), n, P(enc), cap, P(coff), P(est), sp))
+            if ev:
+                ev[1].record(stream)
+            check(lib.tdt_decode_batch(h, P(enc), P(coff), n, P(dec), payload, P(cdoff), P(dst), sp))
+            if ev:
+                ev[2].record(stream)
+
+        cstep()
+        torch.cuda.synchronize(dev)
+        cok = bool(torch.equal(dec, data)) and int(est.abs().sum()) == 0 and int(dst.abs().sum()) == 0
+        cok = cok and int(coff[-1].item()) == enc_bytes and bool(torch.equal(cdoff, off - off[0]))
+        cev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(a.compacted_steps)]
+        for k in range(a.compacted_steps):
+            cstep(cev[k])
+        torch.cuda.synchronize(dev)
+        c_enc = sum(e[0].elapsed_time(e[1]) for e in cev) / a.compacted_steps
+        c_dec = sum(e[1].elapsed_time(e[2]) for e in cev) / a.compacted_steps
+        compacted = {"api": "tdt_encode_batch / tdt_decode_batch (outputs compacted in message order: one pass "
+                            "with decoupled look-back when every message is <= 64 KiB, else slotted kernels + "
+                            "scan of the lengths + gather (decode: sizes + scan, then in place))",
+                     "steps": a.compacted_steps, "encode_ms": round(c_enc, 4), "decode_ms": round(c_dec, 4),
+                     "GiBps_kernels": round(payload / ((c_enc + c_dec) * 1e-3) / 2**30, 3),
+                     "roundtrip_ok": cok, "blob_bytes_equal_slotted": int(coff[-1].item()) == enc_bytes}
+
     host = None
     if a.host_inclusive and a.workload != "c4":
         host = host_inclusive(torch, codec, data, off, n, mb)
@@ -451,6 +489,8 @@ def main():
             "per_rank": per_rank,
             "cpu_baseline": cpu,
         }
+        if compacted:
+            line["compacted"] = compacted
         if host:
             line["host_inclusive"] = host
         if shared:

@@ -106,6 +106,12 @@ struct tdt_ctx {
     // error flags of the host pipeline's chunks, OR-ed since the context was created
     std::atomic<uint32_t> host_flags{0};
     PlanWS pw;                        // the slotted calls' plan workspace
+    // two-phase compacted encode (batches with messages > 64 KiB): slotted blobs, their slots
+    // and lengths, then a scan and a gather into the caller's compacted buffer
+    uint8_t *cp_buf = nullptr;
+    size_t cp_bytes = 0;
+    uint64_t *cp_idx = nullptr;  // slots (n + 1) | lengths (n) | flag
+    size_t cp_idx_n = 0;
     uint64_t large_min = 256 * 1024;  // messages (decode: decoded blobs) above this take the tiled path
     uint32_t tile_cap = ~0u;          // lower tile budget (tests)
 };
@@ -737,6 +743,36 @@ int host_path(tdt_ctx *c, bool encode, const uint8_t *h_in, const uint64_t *h_in
 
 }  // namespace
 
+namespace {
+// any message longer than `lim` bytes → *flag = 1 (one atomic per workgroup)
+__global__ __launch_bounds__(256) void cp_big_kernel(const uint64_t *in_off, uint32_t n, uint64_t lim, uint64_t *flag) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    const bool big = i < n && in_off[i + 1] - in_off[i] > lim;
+    if (__syncthreads_or(big) && threadIdx.x == 0) atomicOr(reinterpret_cast<unsigned long long *>(flag), 1ull);
+}
+// lengths → the scan's input (in place in out_off)
+__global__ __launch_bounds__(256) void cp_len_kernel(const uint64_t *len, uint64_t *out_off, uint32_t n) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i < n) out_off[i] = len[i];
+}
+// blob i: slot → its compacted place (capacity: the reference-visible TDT_E_CAPACITY of the
+// look-back path; out_off keeps the full prefix sum either way)
+__global__ __launch_bounds__(256) void cp_gather_kernel(const uint8_t *src, const uint64_t *slot, const uint64_t *len,
+                                                      uint8_t *dst, const uint64_t *out_off, uint64_t cap,
+                                                      int32_t *status, uint32_t n) {
+    const uint32_t i = blockIdx.x;
+    if (i >= n) return;
+    const uint64_t o = out_off[i], l = len[i];
+    if (o + l > cap) {
+        if (threadIdx.x == 0 && status && status[i] == 0) status[i] = TDT_E_CAPACITY;
+        return;
+    }
+    psy::team_copy_g2g<256>(dst + o, src + slot[i], l);
+}
+}  // namespace
+
+static int scan_sizes(tdt_ctx *ctx, uint64_t *d_off, uint32_t n_msgs, hipStream_t stream);
+
 extern "C" {
 
 void tdt_default_config(tdt_config *cfg) {
@@ -773,6 +809,8 @@ void tdt_ctx_destroy(tdt_ctx *ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->ws) (void)hipFree(ctx->ws);
     if (ctx->slot_sums) (void)hipFree(ctx->slot_sums);
+    if (ctx->cp_buf) (void)hipFree(ctx->cp_buf);
+    if (ctx->cp_idx) (void)hipFree(ctx->cp_idx);
     ctx->pw.release();
     if (ctx->h_dev) (void)hipFree(ctx->h_dev);
     for (auto &h : ctx->hs) {
@@ -814,10 +852,66 @@ uint64_t tdt_encode_bound(uint64_t n, int32_t word_size) {
     return std::max<uint64_t>(tdt, n + 4);
 }
 
+
+// Compacted encode.  Batches of messages up to 64 KiB: one pass, offsets by the kernels'
+// decoupled look-back.  Batches with longer messages: a message's size is known only after
+// its whole analysis, and those take far longer than the rest, so successors waiting in the
+// look-back would stall every CU (head-of-line blocking); they are encoded slotted (the
+// message-class kernels), then the lengths are scanned and the blobs gathered into place.
 int tdt_encode_batch(tdt_ctx *ctx, const uint8_t *d_in, const uint64_t *d_in_off, uint32_t n_msgs, uint8_t *d_out,
                      uint64_t out_cap, uint64_t *d_out_off, int32_t *d_status, void *stream) {
-    return encode_common(ctx, psy::MODE_ENCODE, d_in, d_in_off, n_msgs, nullptr, d_out, out_cap, d_out_off, d_status,
-                         nullptr, nullptr, nullptr, stream);
+    if (!ctx || n_msgs == 0 || !d_in_off || !d_out || !d_out_off || (std::getenv("PSYNE_TDT_NO_TWO_PHASE") && *std::getenv("PSYNE_TDT_NO_TWO_PHASE") == '1'))
+        return encode_common(ctx, psy::MODE_ENCODE, d_in, d_in_off, n_msgs, nullptr, d_out, out_cap, d_out_off,
+                             d_status, nullptr, nullptr, nullptr, stream);
+    hipStream_t s = (hipStream_t)stream;
+    HIPCHK(hipSetDevice(ctx->device));
+    uint64_t h3[3];
+    {
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        const size_t need = 2ull * n_msgs + 2;
+        if (need > ctx->cp_idx_n) {
+            if (ctx->cp_idx) HIPCHK(hipFree(ctx->cp_idx));
+            ctx->cp_idx = nullptr;
+            HIPCHK(hipMalloc(&ctx->cp_idx, 8 * need));
+            ctx->cp_idx_n = need;
+        }
+        uint64_t *flag = ctx->cp_idx + 2ull * n_msgs + 1;
+        HIPCHK(hipMemsetAsync(flag, 0, 8, s));
+        hipLaunchKernelGGL(cp_big_kernel, dim3((n_msgs + 255) / 256), dim3(256), 0, s, d_in_off, n_msgs,
+                           (uint64_t)65536, flag);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(&h3[0], flag, 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(&h3[1], d_in_off, 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(&h3[2], d_in_off + n_msgs, 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+    }
+    if (!h3[0])
+        return encode_common(ctx, psy::MODE_ENCODE, d_in, d_in_off, n_msgs, nullptr, d_out, out_cap, d_out_off,
+                             d_status, nullptr, nullptr, nullptr, stream);
+    uint64_t *slot = ctx->cp_idx, *len = ctx->cp_idx + n_msgs + 1;
+    // Σ encode bounds <= 2·(input bytes) + n·(28 + 4·ws) (and >= n + 4 per message)
+    const uint64_t bound = 2 * (h3[2] - h3[1]) + (uint64_t)n_msgs * (28 + 4ull * (uint64_t)ctx->cfg.word_size + 4);
+    {
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        if (bound > ctx->cp_bytes) {
+            if (ctx->cp_buf) HIPCHK(hipFree(ctx->cp_buf));
+            ctx->cp_buf = nullptr;
+            HIPCHK(hipMalloc(&ctx->cp_buf, bound));
+            ctx->cp_bytes = bound;
+        }
+    }
+    int st = tdt_encode_slots(ctx, d_in_off, n_msgs, slot, stream);
+    if (st) return st;
+    st = tdt_encode_batch_into(ctx, d_in, d_in_off, n_msgs, ctx->cp_buf, slot, len, d_status, stream);
+    if (st) return st;
+    hipLaunchKernelGGL(cp_len_kernel, dim3((n_msgs + 255) / 256), dim3(256), 0, s, len, d_out_off, n_msgs);
+    HIPCHK(hipGetLastError());
+    st = scan_sizes(ctx, d_out_off, n_msgs, s);  // exclusive, total at [n]
+    if (st) return st;
+    hipLaunchKernelGGL(cp_gather_kernel, dim3(n_msgs), dim3(256), 0, s, ctx->cp_buf, slot, len, d_out, d_out_off,
+                       out_cap, d_status, n_msgs);
+    HIPCHK(hipGetLastError());
+    return TDT_OK;
 }
 
 int tdt_encode_with_mapping_batch(tdt_ctx *ctx, const uint8_t *d_in, const uint64_t *d_in_off, uint32_t n_msgs,
@@ -833,8 +927,41 @@ int tdt_analyze_batch(tdt_ctx *ctx, const uint8_t *d_in, const uint64_t *d_in_of
                          d_hist, d_entropy, d_mapping, stream);
 }
 
+// Compacted decode.  Decoded sizes are in the headers, so for batches with blobs decoding to
+// more than 64 KiB (look-back head-of-line blocking, as for encode) the output offsets are
+// computed first (sizes + scan) and the blobs decoded by the slotted kernels straight into
+// their compacted places; other batches, and batches over out_cap, take the look-back kernel.
 int tdt_decode_batch(tdt_ctx *ctx, const uint8_t *d_in, const uint64_t *d_in_off, uint32_t n_msgs, uint8_t *d_out,
                      uint64_t out_cap, uint64_t *d_out_off, int32_t *d_status, void *stream) {
+    if (ctx && n_msgs && d_in_off && d_out && d_out_off &&
+        !(std::getenv("PSYNE_TDT_NO_TWO_PHASE") && *std::getenv("PSYNE_TDT_NO_TWO_PHASE") == '1')) {
+        hipStream_t s = (hipStream_t)stream;
+        HIPCHK(hipSetDevice(ctx->device));
+        int st = tdt_decode_slots(ctx, d_in, d_in_off, nullptr, n_msgs, d_out_off, d_status, stream);
+        if (st) return st;
+        uint64_t h2[2];
+        {
+            std::lock_guard<std::mutex> lk(ctx->mu);
+            const size_t need = 2ull * n_msgs + 2;
+            if (need > ctx->cp_idx_n) {
+                if (ctx->cp_idx) HIPCHK(hipFree(ctx->cp_idx));
+                ctx->cp_idx = nullptr;
+                HIPCHK(hipMalloc(&ctx->cp_idx, 8 * need));
+                ctx->cp_idx_n = need;
+            }
+            uint64_t *flag = ctx->cp_idx + 2ull * n_msgs + 1;
+            HIPCHK(hipMemsetAsync(flag, 0, 8, s));
+            hipLaunchKernelGGL(cp_big_kernel, dim3((n_msgs + 255) / 256), dim3(256), 0, s, d_out_off, n_msgs,
+                               (uint64_t)65536, flag);
+            HIPCHK(hipGetLastError());
+            HIPCHK(hipMemcpyAsync(&h2[0], flag, 8, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipMemcpyAsync(&h2[1], d_out_off + n_msgs, 8, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipStreamSynchronize(s));
+        }
+        if (h2[0] && h2[1] <= out_cap)
+            return tdt_decode_batch_into(ctx, d_in, d_in_off, nullptr, n_msgs, d_out, d_out_off, ctx->cp_idx, d_status,
+                                         stream);
+    }
     return decode_common(ctx, false, d_in, d_in_off, n_msgs, d_out, out_cap, d_out_off, nullptr, d_status, stream);
 }
 
@@ -883,24 +1010,9 @@ int tdt_decode_slots(tdt_ctx *ctx, const uint8_t *d_in, const uint64_t *d_in_off
         if (st) return st;
     }
     HIPCHK(hipSetDevice(ctx->device));
-    const uint32_t nb = (n_msgs + psy::kSlotChunk - 1) / psy::kSlotChunk;
-    if (nb > 1) {
-        std::lock_guard<std::mutex> lk(ctx->mu);
-        if (nb > ctx->slot_sums_n) {
-            if (ctx->slot_sums) HIPCHK(hipFree(ctx->slot_sums));
-            ctx->slot_sums = nullptr;
-            HIPCHK(hipMalloc(&ctx->slot_sums, 8ull * nb));
-            ctx->slot_sums_n = nb;
-        }
-        hipLaunchKernelGGL(psy::tdt_slot_sums_kernel, dim3(nb - 1), dim3(psy::kSlotThreads), 0, (hipStream_t)stream,
-                           d_slot_off, ctx->slot_sums, n_msgs);
-        HIPCHK(hipGetLastError());
-    }
-    hipLaunchKernelGGL(psy::tdt_slot_scan_kernel, dim3(nb ? nb : 1), dim3(psy::kSlotThreads), 0, (hipStream_t)stream,
-                       d_slot_off, nb > 1 ? ctx->slot_sums : nullptr, n_msgs);
-    HIPCHK(hipGetLastError());
-    return TDT_OK;
+    return scan_sizes(ctx, d_slot_off, n_msgs, (hipStream_t)stream);
 }
+
 
 int tdt_encode_host(tdt_ctx *ctx, const uint8_t *h_in, const uint64_t *h_in_off, uint32_t n_msgs, uint8_t *h_out,
                     uint64_t out_cap, uint64_t *h_out_off, int32_t *h_status) {
@@ -987,3 +1099,25 @@ int tdt_prof_read(uint64_t *out32) {
 }
 #endif
 }  // extern "C"
+
+// In-place exclusive scan of n sizes (u64) at d_off; d_off[n] = the total.
+static int scan_sizes(tdt_ctx *ctx, uint64_t *d_slot_off, uint32_t n_msgs, hipStream_t stream) {
+    const uint32_t nb = (n_msgs + psy::kSlotChunk - 1) / psy::kSlotChunk;
+    if (nb > 1) {
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        if (nb > ctx->slot_sums_n) {
+            if (ctx->slot_sums) HIPCHK(hipFree(ctx->slot_sums));
+            ctx->slot_sums = nullptr;
+            HIPCHK(hipMalloc(&ctx->slot_sums, 8ull * nb));
+            ctx->slot_sums_n = nb;
+        }
+        hipLaunchKernelGGL(psy::tdt_slot_sums_kernel, dim3(nb - 1), dim3(psy::kSlotThreads), 0, (hipStream_t)stream,
+                           d_slot_off, ctx->slot_sums, n_msgs);
+        HIPCHK(hipGetLastError());
+    }
+    hipLaunchKernelGGL(psy::tdt_slot_scan_kernel, dim3(nb ? nb : 1), dim3(psy::kSlotThreads), 0, (hipStream_t)stream,
+                       d_slot_off, nb > 1 ? ctx->slot_sums : nullptr, n_msgs);
+    HIPCHK(hipGetLastError());
+    return TDT_OK;
+}
+
