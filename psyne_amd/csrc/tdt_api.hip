@@ -927,10 +927,11 @@ int tdt_analyze_batch(tdt_ctx *ctx, const uint8_t *d_in, const uint64_t *d_in_of
                          d_hist, d_entropy, d_mapping, stream);
 }
 
-// Compacted decode.  Decoded sizes are in the headers, so for batches with blobs decoding to
-// more than 64 KiB (look-back head-of-line blocking, as for encode) the output offsets are
-// computed first (sizes + scan) and the blobs decoded by the slotted kernels straight into
-// their compacted places; other batches, and batches over out_cap, take the look-back kernel.
+// Compacted decode.  Decoded sizes are in the headers, so the output offsets are computed
+// first (sizes + scan) and the blobs decoded by the slotted message-class kernels straight into
+// their compacted places (no copy; and no look-back, whose successors stall behind long blobs);
+// batches whose total exceeds out_cap take the look-back kernel, which assigns
+// TDT_E_CAPACITY per blob.
 int tdt_decode_batch(tdt_ctx *ctx, const uint8_t *d_in, const uint64_t *d_in_off, uint32_t n_msgs, uint8_t *d_out,
                      uint64_t out_cap, uint64_t *d_out_off, int32_t *d_status, void *stream) {
     if (ctx && n_msgs && d_in_off && d_out && d_out_off &&
@@ -939,7 +940,7 @@ int tdt_decode_batch(tdt_ctx *ctx, const uint8_t *d_in, const uint64_t *d_in_off
         HIPCHK(hipSetDevice(ctx->device));
         int st = tdt_decode_slots(ctx, d_in, d_in_off, nullptr, n_msgs, d_out_off, d_status, stream);
         if (st) return st;
-        uint64_t h2[2];
+        uint64_t total = 0;
         {
             std::lock_guard<std::mutex> lk(ctx->mu);
             const size_t need = 2ull * n_msgs + 2;
@@ -949,16 +950,10 @@ int tdt_decode_batch(tdt_ctx *ctx, const uint8_t *d_in, const uint64_t *d_in_off
                 HIPCHK(hipMalloc(&ctx->cp_idx, 8 * need));
                 ctx->cp_idx_n = need;
             }
-            uint64_t *flag = ctx->cp_idx + 2ull * n_msgs + 1;
-            HIPCHK(hipMemsetAsync(flag, 0, 8, s));
-            hipLaunchKernelGGL(cp_big_kernel, dim3((n_msgs + 255) / 256), dim3(256), 0, s, d_out_off, n_msgs,
-                               (uint64_t)65536, flag);
-            HIPCHK(hipGetLastError());
-            HIPCHK(hipMemcpyAsync(&h2[0], flag, 8, hipMemcpyDeviceToHost, s));
-            HIPCHK(hipMemcpyAsync(&h2[1], d_out_off + n_msgs, 8, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipMemcpyAsync(&total, d_out_off + n_msgs, 8, hipMemcpyDeviceToHost, s));
             HIPCHK(hipStreamSynchronize(s));
         }
-        if (h2[0] && h2[1] <= out_cap)
+        if (total <= out_cap)
             return tdt_decode_batch_into(ctx, d_in, d_in_off, nullptr, n_msgs, d_out, d_out_off, ctx->cp_idx, d_status,
                                          stream);
     }
