@@ -755,19 +755,44 @@ __global__ __launch_bounds__(256) void cp_len_kernel(const uint64_t *len, uint64
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
     if (i < n) out_off[i] = len[i];
 }
-// blob i: slot → its compacted place (capacity: the reference-visible TDT_E_CAPACITY of the
-// look-back path; out_off keeps the full prefix sum either way)
+// One wave copies one blob: 16-byte aligned stores; each 16-byte chunk read as five aligned
+// dwords and funnel-shifted by the (constant) source misalignment — compacted offsets have any
+// alignment, so a byte loop would be the common case otherwise.
+__device__ __forceinline__ void wave_copy_any(uint8_t *dst, const uint8_t *src, uint64_t len) {
+    const uint32_t lane = (uint32_t)psy::lane_id();
+    uint64_t head = (16 - ((uintptr_t)dst & 15)) & 15;
+    if (head > len) head = len;
+    if (lane < head) dst[lane] = src[lane];
+    const uint64_t nb = (len - head) / 16;
+    const uint8_t *s0 = src + head;
+    const uint32_t sh = (uint32_t)((uintptr_t)s0 & 3) * 8;
+    const uint32_t *sw = reinterpret_cast<const uint32_t *>((uintptr_t)s0 & ~(uintptr_t)3);
+    uint4 *dv = reinterpret_cast<uint4 *>(dst + head);
+    for (uint64_t k = lane; k < nb; k += 64) {
+        const uint32_t *q = sw + 4 * k;
+        const uint32_t w0 = psy::gload<uint32_t>(q), w1 = psy::gload<uint32_t>(q + 1), w2 = psy::gload<uint32_t>(q + 2),
+                       w3 = psy::gload<uint32_t>(q + 3);
+        // (the fifth dword only when misaligned: it may lie past the source's end otherwise)
+        const uint32_t w4 = sh ? psy::gload<uint32_t>(q + 4) : 0u;
+        dv[k] = make_uint4((uint32_t)((((uint64_t)w1 << 32) | w0) >> sh), (uint32_t)((((uint64_t)w2 << 32) | w1) >> sh),
+                           (uint32_t)((((uint64_t)w3 << 32) | w2) >> sh), (uint32_t)((((uint64_t)w4 << 32) | w3) >> sh));
+    }
+    for (uint64_t k = head + 16 * nb + lane; k < len; k += 64) dst[k] = src[k];
+}
+
+// blob i (one wave each, four per workgroup): slot → its compacted place (capacity: the
+// TDT_E_CAPACITY of the look-back path; out_off keeps the full prefix sum either way)
 __global__ __launch_bounds__(256) void cp_gather_kernel(const uint8_t *src, const uint64_t *slot, const uint64_t *len,
                                                       uint8_t *dst, const uint64_t *out_off, uint64_t cap,
                                                       int32_t *status, uint32_t n) {
-    const uint32_t i = blockIdx.x;
+    const uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (i >= n) return;
     const uint64_t o = out_off[i], l = len[i];
     if (o + l > cap) {
-        if (threadIdx.x == 0 && status && status[i] == 0) status[i] = TDT_E_CAPACITY;
+        if ((threadIdx.x & 63) == 0 && status && status[i] == 0) status[i] = TDT_E_CAPACITY;
         return;
     }
-    psy::team_copy_g2g<256>(dst + o, src + slot[i], l);
+    wave_copy_any(dst + o, src + slot[i], l);
 }
 }  // namespace
 
@@ -908,8 +933,8 @@ int tdt_encode_batch(tdt_ctx *ctx, const uint8_t *d_in, const uint64_t *d_in_off
     HIPCHK(hipGetLastError());
     st = scan_sizes(ctx, d_out_off, n_msgs, s);  // exclusive, total at [n]
     if (st) return st;
-    hipLaunchKernelGGL(cp_gather_kernel, dim3(n_msgs), dim3(256), 0, s, ctx->cp_buf, slot, len, d_out, d_out_off,
-                       out_cap, d_status, n_msgs);
+    hipLaunchKernelGGL(cp_gather_kernel, dim3((n_msgs + 3) / 4), dim3(256), 0, s, ctx->cp_buf, slot, len, d_out,
+                       d_out_off, out_cap, d_status, n_msgs);
     HIPCHK(hipGetLastError());
     return TDT_OK;
 }

@@ -21,7 +21,7 @@ timeout -k 10 400 python -u bench.py > "$OUT/bench.log" 2>&1
 rc=$?; tail -1 "$OUT/bench.log" | cut -c1-400; [ $rc -eq 0 ] || exit $rc
 step rocprof
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
-  python3 bench.py --steps 5 --warmup 2 --cpu-seconds 0 > "$OUT/prof_bench.log" 2>&1
+  python3 bench.py --steps 5 --warmup 2 --cpu-seconds 0 --compacted-steps 0 > "$OUT/prof_bench.log" 2>&1
 rc=$?; [ $rc -eq 0 ] || exit $rc
 python3 tools/prof_summary.py "$OUT/prof" "$OUT/kernel_stats.md" "rocprofv3 --kernel-trace --stats: bench.py --steps 5 --warmup 2 ($TAG)" > /dev/null
 step pmc

@@ -4,7 +4,7 @@
 # usage: tools/profile_pmc.sh <outdir> [bench args]   (writes <outdir>/summary.txt + traffic.json)
 set -u
 OUT=${1:-gpurun_out/pmc}; shift || true
-ARGS=${@:-"--steps 1 --warmup 1 --cpu-seconds 0"}
+ARGS=${@:-"--steps 1 --warmup 1 --cpu-seconds 0 --compacted-steps 0"}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 run() {  # name counters...
