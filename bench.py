@@ -417,9 +417,10 @@ def main():
         torch.cuda.synchronize(dev)
         c_enc = sum(e[0].elapsed_time(e[1]) for e in cev) / a.compacted_steps
         c_dec = sum(e[1].elapsed_time(e[2]) for e in cev) / a.compacted_steps
-        compacted = {"api": "tdt_encode_batch / tdt_decode_batch (outputs compacted in message order: one pass "
-                            "with decoupled look-back when every message is <= 64 KiB, else slotted kernels + "
-                            "scan of the lengths + gather (decode: sizes + scan, then in place))",
+        compacted = {"api": "tdt_encode_batch / tdt_decode_batch (outputs compacted in message order; encode: one "
+                            "pass with decoupled look-back for messages <= 64 KiB averaging >= 16 KiB, else "
+                            "slotted kernels + scan of the lengths + gather; decode: sizes + scan, then the "
+                            "slotted kernels in place)",
                      "steps": a.compacted_steps, "encode_ms": round(c_enc, 4), "decode_ms": round(c_dec, 4),
                      "GiBps_kernels": round(payload / ((c_enc + c_dec) * 1e-3) / 2**30, 3),
                      "roundtrip_ok": cok, "blob_bytes_equal_slotted": int(coff[-1].item()) == enc_bytes}

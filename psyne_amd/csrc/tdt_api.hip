@@ -878,11 +878,12 @@ uint64_t tdt_encode_bound(uint64_t n, int32_t word_size) {
 }
 
 
-// Compacted encode.  Batches of messages up to 64 KiB: one pass, offsets by the kernels'
-// decoupled look-back.  Batches with longer messages: a message's size is known only after
-// its whole analysis, and those take far longer than the rest, so successors waiting in the
-// look-back would stall every CU (head-of-line blocking); they are encoded slotted (the
-// message-class kernels), then the lengths are scanned and the blobs gathered into place.
+// Compacted encode.  Batches of medium messages (none over 64 KiB, >= 16 KiB on average): one
+// pass, offsets by the kernels' decoupled look-back.  Batches with longer messages: a message's
+// size is known only after its whole analysis, and those take far longer than the rest, so
+// successors waiting in the look-back would stall every CU (head-of-line blocking); batches of
+// small messages: the per-message ticket / look-back chain bounds the rate.  Both are encoded
+// slotted (the message-class kernels), then the lengths are scanned and the blobs gathered.
 int tdt_encode_batch(tdt_ctx *ctx, const uint8_t *d_in, const uint64_t *d_in_off, uint32_t n_msgs, uint8_t *d_out,
                      uint64_t out_cap, uint64_t *d_out_off, int32_t *d_status, void *stream) {
     if (!ctx || n_msgs == 0 || !d_in_off || !d_out || !d_out_off || (std::getenv("PSYNE_TDT_NO_TWO_PHASE") && *std::getenv("PSYNE_TDT_NO_TWO_PHASE") == '1'))
@@ -910,7 +911,10 @@ int tdt_encode_batch(tdt_ctx *ctx, const uint8_t *d_in, const uint64_t *d_in_off
         HIPCHK(hipMemcpyAsync(&h3[2], d_in_off + n_msgs, 8, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
     }
-    if (!h3[0])
+    // one pass with the look-back for batches of medium messages (all <= 64 KiB, 16 KiB or more
+    // on average); small messages make the per-message ticket and look-back chain the limit
+    // (C2: 12 ms for 1 Mi x 1 KiB), long ones stall it — both take the two phases
+    if (!h3[0] && (h3[2] - h3[1]) >= 16384ull * n_msgs)
         return encode_common(ctx, psy::MODE_ENCODE, d_in, d_in_off, n_msgs, nullptr, d_out, out_cap, d_out_off,
                              d_status, nullptr, nullptr, nullptr, stream);
     uint64_t *slot = ctx->cp_idx, *len = ctx->cp_idx + n_msgs + 1;

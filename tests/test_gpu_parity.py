@@ -321,8 +321,14 @@ def test_roundtrip_many_64k():
         assert e[eo[i]:eo[i + 1]].tobytes() == want
 
 
-def test_many_tiny_lookback():
-    # 200k UNCP messages: exercises the look-back chain at depth
+@pytest.mark.parametrize("path", ["lookback", "two_phase"])
+def test_many_tiny_lookback(path, monkeypatch):
+    # 200k UNCP messages: the look-back chain at depth (forced: small-message batches take the
+    # two-phase compaction by default) and the two-phase path's scan + gather
+    if path == "lookback":
+        monkeypatch.setenv("PSYNE_TDT_NO_TWO_PHASE", "1")
+    else:
+        monkeypatch.delenv("PSYNE_TDT_NO_TWO_PHASE", raising=False)
     rng = np.random.default_rng(22)
     sizes = rng.integers(0, 40, 200000)
     data = rng.integers(0, 256, int(sizes.sum()), dtype=np.uint8)
