@@ -138,7 +138,12 @@ struct EncLayout {
     // then (pending + up to 64·16 entries) for the two streams together
     static constexpr int WSTAGE_V4 = 2 * WREGION + 16;
     static constexpr int WSTAGE_V5 = 256 + 4 * (2 + 64 * 16);
-    static constexpr int WSTAGE = ((WSTAGE_V4 > WSTAGE_V5 ? WSTAGE_V4 : WSTAGE_V5) + 15) / 16 * 16;
+    // v6 (u16 entries): NB rounds per flush — 3 for message-sized teams (fewer flushes, the LDS
+    // fits 3 workgroups per CU), 2 for the one-wave team (whose LDS sets messages per CU)
+    static constexpr int NB6 = TEAM >= 256 ? 3 : 2;
+    static constexpr int WSTAGE_V6 = 16 + 2 * (3 + NB6 * 64 * 16);
+    static constexpr int WSTAGE_45 = WSTAGE_V4 > WSTAGE_V5 ? WSTAGE_V4 : WSTAGE_V5;
+    static constexpr int WSTAGE = ((WSTAGE_45 > WSTAGE_V6 ? WSTAGE_45 : WSTAGE_V6) + 15) / 16 * 16;
     static constexpr int STAGE = W * WSTAGE;
     static constexpr int TERMS = TEAM >= 256 ? TB * 256 * 16 : 0;  // one-wave teams: in registers
     // Two phases share one region: histogram + entropy terms + log2 tables (dead once the
@@ -1311,13 +1316,14 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
         // Resident messages with word size <= 4: as v5, but entries are u16 (value << 8 |
         // stream position mod 256 — with Ls a multiple of 4 every round starts at a multiple of
         // 256 positions, and consecutive chunk starts are 1..255 apart, so count = (e1 - e0) mod
-        // 256) and TWO rounds share one flush: the per-round flush bookkeeping (pointers, the
+        // 256) and NB rounds (3 for message-sized teams) share one flush: the per-round flush bookkeeping (pointers, the
         // last-entry read, the pending entry, loop set-up) is paid once per pair of rounds.
         constexpr bool E6 = RES && WS <= 4;
         const uint32_t eb6 = wst + 16u;
         // stream 1's u16 region (bytes; a multiple of 4 like eb6, so that every region's even
         // entries are dword-aligned for the flush)
-        const uint32_t eoff6 = 2u * (2u + 128u * L0);
+        constexpr uint32_t NB = Lay::NB6;  // rounds per flush
+        const uint32_t eoff6 = 2u * (2u + NB * 64u * L0);
         uint32_t s6[2] = {0, 0};  // entries of the current batch, per stream
         uint32_t pend6[2] = {0, 0};
 #pragma unroll
@@ -1446,15 +1452,15 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
 #pragma unroll
             for (int r = 0; r < G; ++r) {
                 if ((uint32_t)r < RW) {
-                    if ((r & 1) == 0 && lane == 0) {  // batch start: the pending entries
+                    if (r % NB == 0 && lane == 0) {  // batch start: the pending entries
                         if (hp[0]) *reinterpret_cast<uint16_t *>(smem + eb6) = (uint16_t)pend6[0];
                         if (ns2 && hp[1]) *reinterpret_cast<uint16_t *>(smem + eb6 + eoff6) = (uint16_t)pend6[1];
                     }
 #ifndef PSY_X_NOEMIT
                     sweep6(dres[r], cres[r]);
 #endif
-                    if ((r & 1) == 1 || (uint32_t)(r + 1) == RW) {
-                        const uint32_t gb = gw0 + (uint32_t)(r & ~1) * 64u, ge = gw0 + (uint32_t)r * 64u + 64u;
+                    if (r % NB == NB - 1 || (uint32_t)(r + 1) == RW) {
+                        const uint32_t gb = gw0 + (uint32_t)(r - r % NB) * 64u, ge = gw0 + (uint32_t)r * 64u + 64u;
                         flush6(gb <= ngroups - 1 && ngroups - 1 < ge);
                     }
                 }
