@@ -797,6 +797,15 @@ __global__ __launch_bounds__(256) void cp_gather_kernel(const uint8_t *src, cons
 }  // namespace
 
 static int scan_sizes(tdt_ctx *ctx, uint64_t *d_off, uint32_t n_msgs, hipStream_t stream);
+// The two-phase compaction reads a few bytes back to choose its path: not under stream capture
+// (the one-pass kernels need no read-back), nor with PSYNE_TDT_NO_TWO_PHASE=1.
+static bool two_phase_ok(void *stream) {
+    const char *e = std::getenv("PSYNE_TDT_NO_TWO_PHASE");
+    if (e && *e == '1') return false;
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing((hipStream_t)stream, &cap) != hipSuccess) return false;
+    return cap == hipStreamCaptureStatusNone;
+}
 
 extern "C" {
 
@@ -886,7 +895,7 @@ uint64_t tdt_encode_bound(uint64_t n, int32_t word_size) {
 // slotted (the message-class kernels), then the lengths are scanned and the blobs gathered.
 int tdt_encode_batch(tdt_ctx *ctx, const uint8_t *d_in, const uint64_t *d_in_off, uint32_t n_msgs, uint8_t *d_out,
                      uint64_t out_cap, uint64_t *d_out_off, int32_t *d_status, void *stream) {
-    if (!ctx || n_msgs == 0 || !d_in_off || !d_out || !d_out_off || (std::getenv("PSYNE_TDT_NO_TWO_PHASE") && *std::getenv("PSYNE_TDT_NO_TWO_PHASE") == '1'))
+    if (!ctx || n_msgs == 0 || !d_in_off || !d_out || !d_out_off || !two_phase_ok(stream))
         return encode_common(ctx, psy::MODE_ENCODE, d_in, d_in_off, n_msgs, nullptr, d_out, out_cap, d_out_off,
                              d_status, nullptr, nullptr, nullptr, stream);
     hipStream_t s = (hipStream_t)stream;
@@ -963,8 +972,7 @@ int tdt_analyze_batch(tdt_ctx *ctx, const uint8_t *d_in, const uint64_t *d_in_of
 // TDT_E_CAPACITY per blob.
 int tdt_decode_batch(tdt_ctx *ctx, const uint8_t *d_in, const uint64_t *d_in_off, uint32_t n_msgs, uint8_t *d_out,
                      uint64_t out_cap, uint64_t *d_out_off, int32_t *d_status, void *stream) {
-    if (ctx && n_msgs && d_in_off && d_out && d_out_off &&
-        !(std::getenv("PSYNE_TDT_NO_TWO_PHASE") && *std::getenv("PSYNE_TDT_NO_TWO_PHASE") == '1')) {
+    if (ctx && n_msgs && d_in_off && d_out && d_out_off && two_phase_ok(stream)) {
         hipStream_t s = (hipStream_t)stream;
         HIPCHK(hipSetDevice(ctx->device));
         int st = tdt_decode_slots(ctx, d_in, d_in_off, nullptr, n_msgs, d_out_off, d_status, stream);

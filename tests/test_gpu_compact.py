@@ -117,3 +117,37 @@ def test_two_phase_capacity_semantics():
     for i in range(len(msgs)):
         if s1[i] == 0:
             assert np.array_equal(b1[o1[i]:o1[i + 1]], b2[o2[i]:o2[i + 1]])
+
+
+def test_compacted_under_graph_capture():
+    """Under hipGraph stream capture the compacted API takes the one-pass look-back kernels
+    (the two-phase path reads back on the host); the replayed graph gives the eager bytes."""
+    codec = _codec()
+    msgs, data, off = _batch(4)
+    d = torch.from_numpy(data).cuda()
+    o = torch.from_numpy(off).cuda()
+    ref, roff, rst = codec.encode_batch(d, o)          # eager (two-phase), also sizes the scratch
+    torch.cuda.synchronize()
+    out = torch.zeros_like(ref)
+    eoff = torch.empty_like(roff)
+    st = torch.empty_like(rst)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):                        # warm the look-back path's scratch
+        os.environ["PSYNE_TDT_NO_TWO_PHASE"] = "1"
+        try:
+            codec.encode_batch(d, o, out=out, out_offsets=eoff, status=st)
+        finally:
+            os.environ.pop("PSYNE_TDT_NO_TWO_PHASE", None)
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    out.zero_()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        codec.encode_batch(d, o, out=out, out_offsets=eoff, status=st)
+    g.replay()
+    torch.cuda.synchronize()
+    assert (st.cpu().numpy() == 0).all()
+    assert np.array_equal(eoff.cpu().numpy(), roff.cpu().numpy())
+    n = int(roff[-1].item())
+    assert np.array_equal(out[:n].cpu().numpy(), ref[:n].cpu().numpy())
