@@ -61,7 +61,15 @@ struct PlanWS {
     uint8_t *elarge = nullptr;  // encode: LMeta | tile entries | tile records | span entries | span bins
     uint8_t *dlarge = nullptr;  // decode: DMeta | block entries | block sums | tile entries | tile blocks
     uint32_t *host = nullptr;   // pinned: the plan's counts
+    // the large-message pipeline runs on `side` beside the medium/small lists (fork/join events)
+    hipStream_t side = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
     void release() {
+        if (join) (void)hipEventDestroy(join);
+        if (fork) (void)hipEventDestroy(fork);
+        if (side) (void)hipStreamDestroy(side);
+        side = nullptr;
+        fork = join = nullptr;
         if (buf) (void)hipFree(buf);
         if (elarge) (void)hipFree(elarge);
         if (dlarge) (void)hipFree(dlarge);
@@ -184,6 +192,27 @@ int ensure_plan(PlanWS &w, uint32_t n) {
     return TDT_OK;
 }
 
+// fork `s` onto the side stream (high priority: the tile pipeline is a chain of dependent
+// kernels; the independent medium/small lists fill the CUs it leaves idle at each boundary)
+int fork_side(PlanWS &w, hipStream_t s) {
+    if (std::getenv("PSYNE_TDT_NO_SIDE")) return -1;
+    if (!w.side) {
+        int lo = 0, hi = 0;
+        HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        HIPCHK(hipStreamCreateWithPriority(&w.side, hipStreamNonBlocking, hi));
+        HIPCHK(hipEventCreateWithFlags(&w.fork, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&w.join, hipEventDisableTiming));
+    }
+    HIPCHK(hipEventRecord(w.fork, s));
+    HIPCHK(hipStreamWaitEvent(w.side, w.fork, 0));
+    return TDT_OK;
+}
+int join_side(PlanWS &w, hipStream_t s) {
+    HIPCHK(hipEventRecord(w.join, w.side));
+    HIPCHK(hipStreamWaitEvent(s, w.join, 0));
+    return TDT_OK;
+}
+
 int ensure_elarge(PlanWS &w, int ws) {
     if (!w.elarge) {
         const size_t b = large_bytes(ws);
@@ -239,7 +268,13 @@ int launch_slotted(tdt_ctx *c, PlanWS &pw, psy::EncodeArgs a, hipStream_t s) {
         nsp = (uint32_t)std::min<uint64_t>(h[4], tcap / psy::kSpanTiles);
     }
     // large messages: span histograms, mapping, tile counts, scan, emit
+    bool forked = false;
     if (nt) {
+        const int fr = fork_side(pw, s);
+        if (fr > 0) return fr;
+        forked = fr == TDT_OK;
+        hipStream_t s0 = s;
+        if (forked) s = pw.side;
         a.tiles = tiles;
         a.tile_count = cnt + 6;
         a.tile_cap = tcap;
@@ -253,6 +288,7 @@ int launch_slotted(tdt_ctx *c, PlanWS &pw, psy::EncodeArgs a, hipStream_t s) {
         hipLaunchKernelGGL((psy::tdt_encode_kernel<WS, 512, 8, psy::MODE_ENCODE, 0, 2>), dim3(nt), dim3(512), 0, s, a);
         hipLaunchKernelGGL((psy::tdt_encode_lscan_kernel<WS>), dim3(nl), dim3(64), 0, s, a, cnt + 4, lmax);
         hipLaunchKernelGGL((psy::tdt_encode_kernel<WS, 512, 8, psy::MODE_ENCODE, 0, 3>), dim3(nt), dim3(512), 0, s, a);
+        s = s0;
     }
     // medium, then small messages: one workgroup per list entry
     a.list = mlist;
@@ -267,6 +303,7 @@ int launch_slotted(tdt_ctx *c, PlanWS &pw, psy::EncodeArgs a, hipStream_t s) {
         a.list_base = b;
         hipLaunchKernelGGL((psy::tdt_encode_kernel<WS, 64, 4, psy::MODE_ENCODE, 0, 0>), dim3(g), dim3(64), 0, s, a);
     });
+    if (forked) return join_side(pw, s);
     return TDT_OK;
 }
 
@@ -431,12 +468,19 @@ int launch_decode_slotted(tdt_ctx *c, PlanWS &pw, psy::DecodeArgs a, hipStream_t
     a.bsum = bsum;
     a.tent = tent;
     a.tblk = tblk;
+    bool forked = false;
     if (nl) {
+        const int fr = fork_side(pw, s);
+        if (fr > 0) return fr;
+        forked = fr == TDT_OK;
+        hipStream_t s0 = s;
+        if (forked) s = pw.side;
         hipLaunchKernelGGL(psy::tdt_decode_lprep_kernel, dim3(nl), dim3(256), 0, s, a);
         if (nb) hipLaunchKernelGGL(psy::tdt_decode_lblock_kernel, dim3((nb + 3) / 4), dim3(256), 0, s, a, nb);
         hipLaunchKernelGGL(psy::tdt_decode_lscan_kernel, dim3(nl, 2), dim3(64), 0, s, a);
         a.list_base = 0;
         hipLaunchKernelGGL(psy::tdt_decode_ltile_kernel, dim3(nt), dim3(64), 0, s, a);
+        s = s0;
     }
     launch_list(nn, 64, [&](uint32_t b, uint32_t g) {
         a.list_base = b;
@@ -448,6 +492,7 @@ int launch_decode_slotted(tdt_ctx *c, PlanWS &pw, psy::DecodeArgs a, hipStream_t
         a.list_base = b;
         hipLaunchKernelGGL((psy::tdt_decode_kernel<0, 1>), dim3(g), dim3(64), 0, s, a);
     });
+    if (forked) return join_side(pw, s);
     return TDT_OK;
 }
 
