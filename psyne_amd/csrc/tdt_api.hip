@@ -297,11 +297,14 @@ int launch_slotted(tdt_ctx *c, PlanWS &pw, psy::EncodeArgs a, hipStream_t s) {
         a.list_base = b;
         hipLaunchKernelGGL((psy::tdt_encode_kernel<WS, 512, 8, psy::MODE_ENCODE, 0, 0>), dim3(g), dim3(512), 0, s, a);
     });
+    // small messages behind the tile pipeline on the side stream (the two streams' loads balance
+    // better: C4's tile pipeline is shorter than its medium list)
+    const hipStream_t ss = forked && !std::getenv("PSYNE_TDT_SMALL_MAIN") ? pw.side : s;
     a.list = slist;
     a.list_count = cnt;
     launch_list(ns, 64, [&](uint32_t b, uint32_t g) {
         a.list_base = b;
-        hipLaunchKernelGGL((psy::tdt_encode_kernel<WS, 64, 4, psy::MODE_ENCODE, 0, 0>), dim3(g), dim3(64), 0, s, a);
+        hipLaunchKernelGGL((psy::tdt_encode_kernel<WS, 64, 4, psy::MODE_ENCODE, 0, 0>), dim3(g), dim3(64), 0, ss, a);
     });
     if (forked) return join_side(pw, s);
     return TDT_OK;
@@ -487,10 +490,11 @@ int launch_decode_slotted(tdt_ctx *c, PlanWS &pw, psy::DecodeArgs a, hipStream_t
         hipLaunchKernelGGL((psy::tdt_decode_kernel<0>), dim3(g), dim3(64), 0, s, a);
     });
     // small blobs: one-round windows (a third less LDS per wave: more blobs in flight per CU)
+    const hipStream_t ss = forked && !std::getenv("PSYNE_TDT_SMALL_MAIN") ? pw.side : s;
     a.list = slist;
     launch_list(ns, 64, [&](uint32_t b, uint32_t g) {
         a.list_base = b;
-        hipLaunchKernelGGL((psy::tdt_decode_kernel<0, 1>), dim3(g), dim3(64), 0, s, a);
+        hipLaunchKernelGGL((psy::tdt_decode_kernel<0, 1>), dim3(g), dim3(64), 0, ss, a);
     });
     if (forked) return join_side(pw, s);
     return TDT_OK;
