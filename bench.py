@@ -65,18 +65,53 @@ def parse():
     ap.add_argument("--compacted-steps", type=int, default=3,
                     help="timed steps of the compacted (look-back) API leg after the headline (0 = skip)")
     ap.add_argument("--seed", type=int, default=None)
-    ap.add_argument("--workload", choices=["c2", "c3", "c4"], default="c3",
+    ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5"], default="c3",
                     help="c3 (default, the BASELINE metric): 262,144 x 64 KiB gradient; c2: 1 Mi x 1 KiB "
-                         "uniform bytes; c4: 4 Mi Zipf(1.5)-sized (64 B - 1 MiB) gradient messages")
+                         "uniform bytes; c4: 4 Mi Zipf(1.5)-sized (64 B - 1 MiB) gradient messages; c5: "
+                         "32 GiB of C3-style messages per GPU (256 GiB at 8 GPUs), host-inclusive leg on")
     a = ap.parse_args()
     if a.workload == "c2":
         a.msgs = a.msgs if a.msgs != 262144 else 1 << 20
         a.msg_bytes = 1024 if a.msg_bytes == 65536 else a.msg_bytes
     if a.workload == "c4" and a.msgs == 262144:
         a.msgs = 1 << 22
+    if a.workload == "c5":
+        if a.msgs == 262144:
+            a.msgs = (32 << 30) // a.msg_bytes  # 32 GiB per GPU
+        a.host_inclusive = True
+        a.compacted_steps = 0  # (its staging buffer would add 2x the payload again)
     if a.seed is None:
-        a.seed = {"c2": 0x5EED0001, "c3": 0x5EED0002, "c4": 0x5EED0003}[a.workload]
+        a.seed = {"c2": 0x5EED0001, "c3": 0x5EED0002, "c4": 0x5EED0003, "c5": 0x5EED0005}[a.workload]
     return a
+
+
+def free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(a) -> int:
+    """`bench.py --gpus N` outside a torch.distributed launch: start N ranks (one process per GPU)
+    as a child `torch.distributed.run` BEFORE this process touches the GPU, relay its output and
+    return its exit code.  (The child ranks see WORLD_SIZE == N and run main().)"""
+    shared = os.environ.get("PSYNE_BENCH_SHARED_DEVICE") == "1"
+    if not shared:
+        import torch  # device_count() does not initialise the GPU on this image
+        have = torch.cuda.device_count()
+        if have < a.gpus:
+            print("bench.py: --gpus %d but only %d visible GPU(s)" % (a.gpus, have), file=sys.stderr, flush=True)
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(a.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), str(ROOT / "bench.py")] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "16")
+    sys.stdout.flush()
+    return subprocess.run(cmd, cwd=str(ROOT), env=env).returncode  # rank 0's JSON line goes to our stdout
 
 
 def gen_gradient(torch, n_msgs, msg_bytes, seed, device):
@@ -279,10 +314,15 @@ def gather_obj(obj, world):
 
 def main():
     a = parse()
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(launch_ranks(a))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != a.gpus:
+        print("bench.py: --gpus %d but WORLD_SIZE=%d" % (a.gpus, world), file=sys.stderr, flush=True)
+        sys.exit(2)
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # PSYNE_BENCH_SHARED_DEVICE=1: rehearsal of the N-rank path on a one-GPU box (every rank on
@@ -299,6 +339,13 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     red = None if shared else dev  # where the reduction tensors live (gloo: host)
+    observed_world = dist.get_world_size() if world > 1 else 1
+    if observed_world != a.gpus:
+        raise SystemExit("bench.py: process group has %d ranks, --gpus %d" % (observed_world, a.gpus))
+    props = torch.cuda.get_device_properties(dev)
+    my_dev = {"local_rank": local, "name": props.name, "arch": getattr(props, "gcnArchName", ""),
+              "pci": "%04x:%02x:%02x" % (getattr(props, "pci_domain_id", 0), getattr(props, "pci_bus_id", 0),
+                                          getattr(props, "pci_device_id", 0))}
 
     from psyne_amd import TDTConfig, TdtCodec
     from psyne_amd.shard import all_true, reduce_max, reduce_sum
@@ -429,7 +476,8 @@ def main():
     if a.host_inclusive and a.workload != "c4":
         host = host_inclusive(torch, codec, data, off, n, mb)
         host["pcie_ceiling"] = pcie_ceiling(torch, dev)
-    per_rank = gather_obj({"rank": rank, "GiBps": round(my_rate, 3), "kernels_ms": [round(t_enc, 4), round(t_dec, 4)],
+    per_rank = gather_obj({"rank": rank, "device": my_dev, "msgs": n, "payload_bytes": payload,
+                           "GiBps": round(my_rate, 3), "kernels_ms": [round(t_enc, 4), round(t_dec, 4)],
                            "host_inclusive": host}, world)
 
     if rank == 0:
@@ -449,6 +497,12 @@ def main():
             metric = "TDT encode+decode GiB/s (device-resident), 64 KiB msgs, 1/2/4/8 MI355X"
             workload = "C3: %d x %d B float32 gradient-like messages per GPU, encode+decode" % (n, mb)
             data_desc = "synthetic (device-generated gradient-like float32: 70% zeros, N(0,0.01); seed 0x5EED0002+rank)"
+        elif a.workload == "c5":
+            metric = "TDT encode+decode GiB/s (device-resident), 64 KiB msgs, 32 GiB per GPU stream"
+            workload = ("C5: %d x %d B (%.1f GiB) C3-style gradient messages per GPU, %.1f GiB job, encode+decode"
+                        % (n, mb, payload / 2**30, job_payload / 2**30))
+            data_desc = ("synthetic (device-generated gradient-like float32, resident in HBM: %.0f GB per GPU "
+                         "incl. slots; seed 0x5EED0005+rank)" % ((payload * 2 + cap) / 1e9))
         elif a.workload == "c2":
             metric = "TDT encode+decode GiB/s (device-resident), 1 KiB uniform msgs"
             workload = "C2: %d x %d B uniform random messages per GPU, encode+decode" % (n, mb)
@@ -463,6 +517,7 @@ def main():
             "value": round(value, 3),
             "unit": "GiB/s",
             "n_gpus": world,
+            "world_size_observed": observed_world,
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": round(ms_per_step, 4),

@@ -5,6 +5,7 @@ CPU oracle (test infrastructure, standing in for the GPU codec), and the gathere
 equal the single-process encoding byte for byte; the bench's max-over-ranks time and
 all-ranks-ok reductions are exercised on the same group."""
 import os
+import pathlib
 import socket
 
 import numpy as np
@@ -91,3 +92,15 @@ def test_two_rank_gloo_shards_match_single_process():
     flat = [blob for shard in gathered for blob in shard]
     assert flat == single
     assert bounds[0] == 0 and bounds[-1] == len(msgs) and 0 < bounds[1] < len(msgs)
+
+
+def test_bench_refuses_world_size_mismatch():
+    """bench.py --gpus N must run exactly N ranks: a launch of another size exits non-zero
+    before touching a GPU (the driver's SCALE points would be mislabelled otherwise)."""
+    import subprocess
+    import sys
+    root = pathlib.Path(__file__).resolve().parents[1]
+    env = dict(os.environ, WORLD_SIZE="3", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, "bench.py", "--gpus", "2"], cwd=root, env=env, capture_output=True,
+                       text=True, timeout=120)
+    assert p.returncode == 2 and "WORLD_SIZE=3" in p.stderr

@@ -102,16 +102,24 @@ def test_two_ranks_hip_codec_shards_match_oracle():
 
 
 @pytest.mark.timeout(240)
-def test_bench_two_ranks_shared_device():
+@pytest.mark.parametrize("launcher", ["plain", "torchrun"])
+def test_bench_two_ranks_shared_device(launcher):
+    """`python bench.py --gpus 2` (what the driver runs) must start two ranks itself; under an
+    explicit torch.distributed.run it must join the launched ranks."""
     env = dict(os.environ, PSYNE_BENCH_SHARED_DEVICE="1", OMP_NUM_THREADS="4")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
-           "--msgs", "4096", "--steps", "2", "--warmup", "1", "--cpu-seconds", "0"]
+    env.pop("WORLD_SIZE", None)
+    args = ["bench.py", "--gpus", "2", "--msgs", "4096", "--steps", "2", "--warmup", "1", "--cpu-seconds", "0"]
+    if launcher == "plain":
+        cmd = [sys.executable] + args
+    else:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port())] + args
     p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=220)
     assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, p.stdout
     r = json.loads(lines[0])
-    assert r["n_gpus"] == 2 and r["roundtrip_ok"] is True
+    assert r["n_gpus"] == 2 and r["world_size_observed"] == 2 and r["roundtrip_ok"] is True
     assert [x["rank"] for x in r["per_rank"]] == [0, 1]
+    assert all(x["device"]["local_rank"] == 0 for x in r["per_rank"])  # shared-device rehearsal
     assert r["value"] > 0 and r["cpu_baseline"] is None
