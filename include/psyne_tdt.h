@@ -66,6 +66,8 @@ extern "C" {
 #define TDT_E_CONFIG 8        /* invalid tdt_config */
 #define TDT_E_HIP 10          /* HIP runtime error (tdt_last_error has the text) */
 #define TDT_E_ARG 11          /* invalid argument */
+#define TDT_E_CAPTURE 12      /* a workspace must grow while the stream is captured: make one eager
+                                 call of the batch on this context before capturing it */
 
 /* TDTConfig (:31-43).  Fields the reference declares but never reads
  * (auto_detect_clusters, max_clusters, enable_simd) are omitted. */
@@ -158,21 +160,37 @@ int tdt_analyze_batch(tdt_ctx *ctx, const uint8_t *d_in, const uint64_t *d_in_of
                       uint32_t *d_hist, double *d_entropy, int32_t *d_mapping, int32_t *d_status,
                       void *hip_stream);
 
-/* Host-memory convenience path (the TCP socket-buffer case): pinned staging, H2D, the batch
- * kernel, D2H, synchronise.  h_out must hold the sum of tdt_encode_bound (encode) or of the
- * decoded sizes (decode); h_out_off receives n+1 offsets.  Blocks the calling thread. */
+/* Host-memory path (the TCP socket-buffer case).  The batch runs as 64 MiB chunks on two
+ * streams (H2D, kernel and D2H of neighbouring chunks overlap).  Pinned caller buffers are DMA'd
+ * directly; pageable ones (std::vector, numpy) are staged through the context's pinned buffers
+ * by a pool of host threads (TDT_OPT_COPY_THREADS).  h_out must hold the sum of
+ * tdt_encode_bound (encode) or of the decoded sizes (decode); h_out_off receives n+1 offsets.
+ * Blocks the calling thread until the results are in h_out. */
 int tdt_encode_host(tdt_ctx *ctx, const uint8_t *h_in, const uint64_t *h_in_off, uint32_t n_msgs,
                     uint8_t *h_out, uint64_t out_cap, uint64_t *h_out_off, int32_t *h_status);
 int tdt_decode_host(tdt_ctx *ctx, const uint8_t *h_in, const uint64_t *h_in_off, uint32_t n_msgs,
                     uint8_t *h_out, uint64_t out_cap, uint64_t *h_out_off, int32_t *h_status);
 
-/* Device-side invariant flags (synchronises the device): bit0 look-back timeout, bit1
- * staging-index guard, bit2 flush-bound guard.  Always 0 for a correct build; the guards turn
- * a logic error into a flag instead of a wild write.  Scope: the most recent compacted
- * (look-back) batch on the context's workspace, OR-ed with every slotted batch since then
- * (slotted calls do not clear the word) and with every host-pipeline chunk since the context
- * was created (sticky). */
-int tdt_ctx_error_flags(tdt_ctx *ctx, uint32_t *flags);
+/* Device-side invariant flags: bit0 look-back timeout, bit1 staging-index guard, bit2
+ * flush-bound guard.  Always 0 for a correct build; the guards turn a logic error into a flag
+ * instead of a wild write.  Reads the flag word in stream order on `hip_stream` (the stream
+ * the context's batches were issued on) and synchronises that stream only.  Scope: the most
+ * recent compacted (look-back) batch on the context's workspace, OR-ed with every slotted
+ * batch since then (slotted calls do not clear the word) and with every host-pipeline chunk
+ * since the context was created (sticky). */
+int tdt_ctx_error_flags(tdt_ctx *ctx, void *hip_stream, uint32_t *flags);
+
+/* Tuning / diagnostic options (tdt_ctx_create reads the same from the environment once:
+ * PSYNE_TDT_LARGE_MIN, PSYNE_TDT_TILE_CAP, PSYNE_TDT_NO_SIDE, PSYNE_TDT_SMALL_MAIN,
+ * PSYNE_TDT_NO_TWO_PHASE).  Not needed for correct results: every setting encodes and decodes
+ * the same bytes. */
+#define TDT_OPT_LARGE_MIN 1               /* messages above this many bytes take the tiled path */
+#define TDT_OPT_TILE_CAP 2                /* lower tile budget per batch (tests of the fallback) */
+#define TDT_OPT_NO_SIDE_STREAM 3          /* 1: the tile pipeline runs on the caller's stream */
+#define TDT_OPT_SMALL_ON_CALLER_STREAM 4  /* 1: small-message lists stay on the caller's stream */
+#define TDT_OPT_NO_TWO_PHASE 5            /* 1: compacted calls always take the one-pass kernels */
+#define TDT_OPT_COPY_THREADS 6            /* host threads staging pageable buffers (default <= 8) */
+int tdt_ctx_set_option(tdt_ctx *ctx, int option, uint64_t value);
 
 /* Host-memory analyze (analyze_data :206-222): h_entropy n*ws doubles, h_mapping n*ws int32
  * (either may be NULL).  Blocks the calling thread. */

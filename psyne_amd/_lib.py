@@ -13,7 +13,9 @@ LIB_PATH = pathlib.Path(__file__).resolve().parent / "libpsyne_tdt.so"
 
 TDT_OK, TDT_E_SHORT, TDT_E_MAGIC, TDT_E_TRUNCATED, TDT_E_BAD_MAPPING = 0, 1, 2, 3, 4
 TDT_E_CAPACITY, TDT_E_UNSUPPORTED, TDT_E_BAD_HEADER, TDT_E_CONFIG = 5, 6, 7, 8
-TDT_E_HIP, TDT_E_ARG = 10, 11
+TDT_E_HIP, TDT_E_ARG, TDT_E_CAPTURE = 10, 11, 12
+TDT_OPT_LARGE_MIN, TDT_OPT_TILE_CAP, TDT_OPT_NO_SIDE_STREAM = 1, 2, 3
+TDT_OPT_SMALL_ON_CALLER_STREAM, TDT_OPT_NO_TWO_PHASE, TDT_OPT_COPY_THREADS = 4, 5, 6
 
 
 class TdtConfigC(C.Structure):
@@ -49,7 +51,8 @@ SIGNATURES = {
     "tdt_encode_host": (C.c_int, [_vp, _vp, _vp, C.c_uint32, _vp, C.c_uint64, _vp, _vp]),
     "tdt_decode_host": (C.c_int, [_vp, _vp, _vp, C.c_uint32, _vp, C.c_uint64, _vp, _vp]),
     "tdt_analyze_host": (C.c_int, [_vp, _vp, _vp, C.c_uint32, _vp, _vp, _vp]),
-    "tdt_ctx_error_flags": (C.c_int, [_vp, C.POINTER(C.c_uint32)]),
+    "tdt_ctx_error_flags": (C.c_int, [_vp, _vp, C.POINTER(C.c_uint32)]),
+    "tdt_ctx_set_option": (C.c_int, [_vp, C.c_int, C.c_uint64]),
     "tdt_last_error": (C.c_char_p, []),
     "tdt_status_string": (C.c_char_p, [C.c_int]),
 }

@@ -12,10 +12,13 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <mutex>
+#include <sched.h>
 #include <string>
 #include <vector>
 
+#include "tdt_copypool.h"
 #include "tdt_decode.h"
 #include "tdt_encode.h"
 #include "tdt_slots.h"
@@ -23,8 +26,8 @@
 // The encode kernels live in tdt_enc_ws.hip (one translation unit per word size); diagnostic
 // builds (word size 4 only, phase profiling) instantiate them here instead.
 #if !defined(PSY_FAST_BUILD) && !(defined(PSY_PROF) && PSY_PROF) && !defined(PSY_SINGLE_TU)
-#define PSY_ENC_EXT(WS, T, G, M, L, TL) \
-    extern template __global__ void psy::tdt_encode_kernel<WS, T, G, psy::M, L, TL>(psy::EncodeArgs);
+#define PSY_ENC_EXT(WS, T, G, M, L, TL, PS) \
+    extern template __global__ void psy::tdt_encode_kernel<WS, T, G, psy::M, L, TL, PS>(psy::EncodeArgs);
 #define PSY_ENC_EXT_WS(WS)                 \
     PSY_ENC_INSTANCES(PSY_ENC_EXT, WS)     \
     extern template __global__ void psy::tdt_encode_lscan_kernel<WS>(psy::EncodeArgs, const uint32_t *, uint32_t);
@@ -51,16 +54,58 @@ int set_err(int code, const std::string &msg) {
             return set_err(TDT_E_HIP, std::string(#expr ": ") + hipGetErrorString(e_));    \
     } while (0)
 
+bool capturing(hipStream_t s) {
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    return hipStreamIsCapturing(s, &cap) == hipSuccess && cap != hipStreamCaptureStatusNone;
+}
+// A workspace must grow: not possible while the stream is being captured (the allocator and
+// the implicit synchronisation of a free are not capturable) — warm the context with one eager
+// call of the batch first.
+int no_growth_in_capture(hipStream_t s) {
+    if (!capturing(s)) return TDT_OK;
+    return set_err(TDT_E_CAPTURE, "workspace too small for this batch under stream capture: issue one eager call "
+                                  "of the same batch size on this context before capturing");
+}
+
 }  // namespace
+
+// Counts of an earlier plan (the slotted calls size their main grids from them; no call ever
+// waits for them).  Each call's plan counters are copied into pinned memory behind the plan
+// kernel; a later call takes them once that copy has completed.
+struct CountHist {
+    uint32_t *pin = nullptr;  // pinned: the plan's 8 u64 counters
+    hipEvent_t ev = nullptr;
+    bool pending = false, valid = false;
+    uint32_t v[16] = {};
+    // fold the newest completed snapshot in (never waits)
+    void refresh() {
+        if (pending && hipEventQuery(ev) == hipSuccess) {
+            std::memcpy(v, pin, sizeof(v));
+            valid = true;
+            pending = false;
+        }
+    }
+    void release() {
+        if (ev) (void)hipEventDestroy(ev);
+        if (pin) (void)hipHostFree(pin);
+        ev = nullptr;
+        pin = nullptr;
+        pending = valid = false;
+    }
+};
 
 // Workspace of the slotted calls' plan (message classes / large-message state).  One per
 // stream user: the context's own, and one per host-pipeline slot (those run concurrently).
 struct PlanWS {
     uint8_t *buf = nullptr;  // counters | lists (grows with the batch)
     size_t bytes = 0;
+    // large-message state, allocated at a small budget and grown (to the counts a plan reported)
+    // when a batch had more large messages than the budget held
     uint8_t *elarge = nullptr;  // encode: LMeta | tile entries | tile records | span entries | span bins
+    uint32_t e_lcap = 0, e_tcap = 0;
     uint8_t *dlarge = nullptr;  // decode: DMeta | block entries | block sums | tile entries | tile blocks
-    uint32_t *host = nullptr;   // pinned: the plan's counts
+    uint32_t d_lcap = 0, d_bcap = 0, d_tcap = 0;
+    CountHist eh, dh;  // encode / decode plan counts
     // the large-message pipeline runs on `side` beside the medium/small lists (fork/join events)
     hipStream_t side = nullptr;
     hipEvent_t fork = nullptr, join = nullptr;
@@ -73,9 +118,10 @@ struct PlanWS {
         if (buf) (void)hipFree(buf);
         if (elarge) (void)hipFree(elarge);
         if (dlarge) (void)hipFree(dlarge);
-        if (host) (void)hipHostFree(host);
         buf = elarge = dlarge = nullptr;
-        host = nullptr;
+        e_lcap = e_tcap = d_lcap = d_bcap = d_tcap = 0;
+        eh.release();
+        dh.release();
         bytes = 0;
     }
 };
@@ -95,9 +141,10 @@ struct tdt_ctx {
     // like `ws`: one slotted decode per context at a time)
     uint64_t *slot_sums = nullptr;
     uint32_t slot_sums_n = 0;
-    // host-path device buffers (tdt_analyze_host)
+    // host-path device buffers and stream (tdt_analyze_host)
     uint8_t *h_dev = nullptr;
     size_t h_dev_bytes = 0;
+    hipStream_t astream = nullptr;
     // host pipeline (tdt_encode_host / tdt_decode_host): two slots, each with its own stream,
     // device buffer (input, offsets, output, status, look-back workspace) and pinned offsets
     struct HostSlot {
@@ -108,8 +155,12 @@ struct tdt_ctx {
         uint64_t *pin = nullptr;  // pinned: in_off (n+1) | out_off (n+1) | status (n, int32 pairs)
         size_t pin_words = 0;
         uint32_t *flag = nullptr;  // pinned: the last chunk's device error flags
+        uint8_t *stage_in = nullptr, *stage_out = nullptr;  // pinned staging for pageable callers
+        size_t sin_bytes = 0, sout_bytes = 0;
         PlanWS pw;
     } hs[2];
+    std::unique_ptr<CopyPool> pool;  // host threads of the staging copies
+    int copy_threads = 8;
     std::mutex hmu;
     // error flags of the host pipeline's chunks, OR-ed since the context was created
     std::atomic<uint32_t> host_flags{0};
@@ -122,15 +173,21 @@ struct tdt_ctx {
     size_t cp_idx_n = 0;
     uint64_t large_min = 256 * 1024;  // messages (decode: decoded blobs) above this take the tiled path
     uint32_t tile_cap = ~0u;          // lower tile budget (tests)
+    // diagnostic knobs (read once at tdt_ctx_create from the environment, or tdt_ctx_set_option)
+    bool no_side = false;       // PSYNE_TDT_NO_SIDE: no side stream for the tile pipeline
+    bool small_main = false;    // PSYNE_TDT_SMALL_MAIN: small lists on the caller's stream
+    bool no_two_phase = false;  // PSYNE_TDT_NO_TWO_PHASE: compacted calls take the one-pass kernels
+    int cus = 256;              // compute units (overflow grids)
 };
 
 namespace {
 
 constexpr size_t kCounterBytes = 64;
 
-int ensure_ws(tdt_ctx *c, uint32_t n_msgs) {
+int ensure_ws(tdt_ctx *c, uint32_t n_msgs, hipStream_t s) {
     const size_t need = kCounterBytes + 8ull * (n_msgs + 1);
     if (need > c->ws_bytes) {
+        if (int st = no_growth_in_capture(s)) return st;
         if (c->ws) HIPCHK(hipFree(c->ws));
         c->ws = nullptr;
         size_t cap = std::max<size_t>(need, c->ws_bytes * 2);
@@ -163,39 +220,67 @@ int launch_encode_t(psy::EncodeArgs a, hipStream_t s) {
 // ---------------------------------------------------------------------------------------
 // Slotted encode (the hot path): a plan kernel sorts the messages into classes — large
 // messages as 64 KiB tiles (histogram + mapping, count, scan, emit), medium messages one
-// 512-lane team each, small ones one wave each — and the host reads its four counts back
-// (16 bytes; the one synchronisation of the call) to size every grid exactly.  Under stream
-// capture (hipGraphs) the counts cannot be read: the grids then cover every message (surplus
-// workgroups exit at once) and large messages stay medium.
+// 512-lane team each, small ones one wave each — into lists whose lengths stay in device
+// memory.  The host never reads them: each class kernel is launched twice, a main launch of
+// one workgroup per entry whose grid comes from an EARLIER call's counts (CountHist: slack on
+// top; the batch size before any count is known), and an overflow launch that walks the
+// entries past that grid (grid-stride; it exits at once when there are none).  A class that
+// an earlier plan found empty is switched off in the plan (its messages join the medium list,
+// which takes any size), so repeated batches of one shape launch exactly what they need.
+// Calls are therefore asynchronous and capturable (hipGraphs).
 constexpr uint64_t kSmallMax = 4096;  // one-wave teams up to this size
-constexpr uint32_t kLmax = 1u << 16;   // large messages per batch
-// tiles per batch: 256 MiB of span histograms (WS KiB per 512 KiB span) — 32 GiB of large
-// messages at word size 4 (C4's 4 Mi-message Zipf batch holds 12 GiB of them); further large
-// messages in the batch stay medium (one 512-lane team each, streaming: far slower)
+constexpr uint32_t kLmax = 1u << 16;   // large messages per batch (full budget)
+// tiles per batch at the full budget: 256 MiB of span histograms (WS KiB per 512 KiB span) —
+// 32 GiB of large messages at word size 4 (C4's 4 Mi-message Zipf batch holds 12 GiB of them);
+// further large messages in the batch stay medium (one 512-lane team each, streaming)
 uint32_t tile_cap_of(int ws) { return (262144u / (uint32_t)ws) * psy::kSpanTiles; }
-size_t large_bytes(int ws) {
-    const size_t tc = tile_cap_of(ws);
-    return (size_t)kLmax * sizeof(psy::LMeta) + tc * (8 + sizeof(psy::TileRec)) + (tc / psy::kSpanTiles) * 8 +
-           (tc / psy::kSpanTiles) * ws * 1024;
+// the budget a context starts with (512 MiB of large messages); plans that claim more grow it
+constexpr uint32_t kL0 = 1024, kT0 = 8192;
+size_t elarge_bytes(uint32_t lcap, uint32_t tcap, int ws) {
+    const size_t sc = tcap / psy::kSpanTiles;
+    return (size_t)lcap * sizeof(psy::LMeta) + (size_t)tcap * (8 + sizeof(psy::TileRec)) + sc * 8 + sc * ws * 1024;
+}
+uint32_t pow2_at_least(uint64_t x, uint32_t lo, uint32_t hi) {
+    uint64_t p = lo;
+    while (p < x && p < hi) p *= 2;
+    return (uint32_t)std::min<uint64_t>(p, hi);
 }
 
-int ensure_plan(PlanWS &w, uint32_t n) {
+int ensure_plan(PlanWS &w, uint32_t n, hipStream_t s) {
     const size_t need = 256 + 8ull * n;
     if (need > w.bytes) {
+        if (int st = no_growth_in_capture(s)) return st;
         if (w.buf) HIPCHK(hipFree(w.buf));
         w.buf = nullptr;
         const size_t cap = std::max(need, w.bytes * 2);
         HIPCHK(hipMalloc(&w.buf, cap));
         w.bytes = cap;
     }
-    if (!w.host) HIPCHK(hipHostMalloc(&w.host, 256, hipHostMallocDefault));
     return TDT_OK;
+}
+
+// The plan counters of this call → pinned snapshot (not under stream capture).
+int record_counts(CountHist &h, const void *dcnt, hipStream_t s) {
+    if (!h.pin) {
+        HIPCHK(hipHostMalloc(&h.pin, 64, hipHostMallocDefault));
+        HIPCHK(hipEventCreateWithFlags(&h.ev, hipEventDisableTiming));
+    }
+    HIPCHK(hipMemcpyAsync(h.pin, dcnt, 64, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipEventRecord(h.ev, s));
+    h.pending = true;
+    return TDT_OK;
+}
+
+// Main-launch grid of a class: the earlier count plus slack (capped), or `dflt` before any.
+uint32_t guess(const CountHist &h, int idx, uint32_t bound, uint32_t dflt) {
+    if (!h.valid) return std::min(dflt, bound);
+    const uint64_t x = h.v[idx];
+    return (uint32_t)std::min<uint64_t>(x + x / 8 + 64, bound);
 }
 
 // fork `s` onto the side stream (high priority: the tile pipeline is a chain of dependent
 // kernels; the independent medium/small lists fill the CUs it leaves idle at each boundary)
 int fork_side(PlanWS &w, hipStream_t s) {
-    if (std::getenv("PSYNE_TDT_NO_SIDE")) return -1;
     if (!w.side) {
         int lo = 0, hi = 0;
         HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
@@ -212,13 +297,36 @@ int join_side(PlanWS &w, hipStream_t s) {
     HIPCHK(hipStreamWaitEvent(s, w.join, 0));
     return TDT_OK;
 }
+// before a workspace is freed: the work of earlier calls that may still use it has finished
+// (only when a budget grows)
+int drain(PlanWS &w, hipStream_t s) {
+    HIPCHK(hipStreamSynchronize(s));
+    if (w.side) HIPCHK(hipStreamSynchronize(w.side));
+    return TDT_OK;
+}
 
-int ensure_elarge(PlanWS &w, int ws) {
-    if (!w.elarge) {
-        const size_t b = large_bytes(ws);
-        HIPCHK(hipMalloc(&w.elarge, b));
-        HIPCHK(hipMemset(w.elarge, 0, b));
+// Large-message budget: allocated on the first batch that may hold large messages, grown to
+// what an earlier plan claimed.
+int ensure_elarge(PlanWS &w, int ws, hipStream_t s) {
+    uint32_t lc = w.e_lcap ? w.e_lcap : kL0, tc = w.e_tcap ? w.e_tcap : kT0;
+    if (w.eh.valid) {
+        lc = std::max(lc, pow2_at_least(w.eh.v[4], kL0, kLmax));
+        tc = std::max(tc, pow2_at_least(std::max<uint64_t>(w.eh.v[6], (uint64_t)w.eh.v[8] * psy::kSpanTiles), kT0,
+                                        tile_cap_of(ws)));
     }
+    if (w.elarge && lc == w.e_lcap && tc == w.e_tcap) return TDT_OK;
+    if (w.elarge) {
+        int st = drain(w, s);
+        if (st) return st;
+        HIPCHK(hipFree(w.elarge));
+        w.elarge = nullptr;
+        w.e_lcap = w.e_tcap = 0;
+    }
+    const size_t b = elarge_bytes(lc, tc, ws);
+    HIPCHK(hipMalloc(&w.elarge, b));
+    HIPCHK(hipMemsetAsync(w.elarge, 0, b, s));
+    w.e_lcap = lc;
+    w.e_tcap = tc;
     return TDT_OK;
 }
 
@@ -232,80 +340,118 @@ void launch_list(uint32_t count, uint32_t team, F &&launch) {
 
 template <int WS>
 int launch_slotted(tdt_ctx *c, PlanWS &pw, psy::EncodeArgs a, hipStream_t s) {
+    using psy::MODE_ENCODE;
     const uint32_t n = a.n_msgs;
-    int st = ensure_plan(pw, n);
-    if (!st) st = ensure_elarge(pw, WS);
+    int st = ensure_plan(pw, n, s);
     if (st) return st;
+    const bool capturing = ::capturing(s);
+    CountHist &H = pw.eh;
+    if (!capturing) H.refresh();  // (event queries are not capturable)
+    // classes an earlier plan found empty are off (their messages, if any, go medium)
+    const bool small_on = !H.valid || H.v[10] > 0;  // (counter 5: small messages, listed or not)
+    bool tiles_on = !H.valid || H.v[4] > 0;
+    if (tiles_on && !capturing) {
+        st = ensure_elarge(pw, WS, s);
+        if (st) return st;
+    }
+    tiles_on = tiles_on && pw.elarge;
     auto *cnt64 = reinterpret_cast<unsigned long long *>(pw.buf);
     auto *cnt = reinterpret_cast<uint32_t *>(pw.buf);  // cnt[2k]: the low word of counter k
     uint32_t *slist = reinterpret_cast<uint32_t *>(pw.buf + 256), *mlist = slist + n;
-    const uint32_t tfull = tile_cap_of(WS), scap = tfull / psy::kSpanTiles;
-    const uint32_t lmax = kLmax, tcap = std::min(tfull, std::max(c->tile_cap, psy::kSpanTiles));
+    const uint32_t lcap = tiles_on ? pw.e_lcap : 0u;
+    const uint32_t tcap = tiles_on ? std::min(pw.e_tcap, std::max(c->tile_cap, psy::kSpanTiles)) : 0u;
+    const uint32_t scap = tcap / psy::kSpanTiles;
     auto *lmeta = reinterpret_cast<psy::LMeta *>(pw.elarge);
-    auto *tiles = reinterpret_cast<uint64_t *>(pw.elarge + (size_t)lmax * sizeof(psy::LMeta));
-    auto *trec = reinterpret_cast<psy::TileRec *>(reinterpret_cast<uint8_t *>(tiles) + 8ull * tfull);
-    auto *spans = reinterpret_cast<uint64_t *>(reinterpret_cast<uint8_t *>(trec) + sizeof(psy::TileRec) * tfull);
-    auto *shist = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(spans) + 8ull * scap);
-    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-    HIPCHK(hipStreamIsCapturing(s, &cap));
-    const bool capturing = cap != hipStreamCaptureStatusNone;
+    auto *tiles = reinterpret_cast<uint64_t *>(pw.elarge + (size_t)pw.e_lcap * sizeof(psy::LMeta));
+    auto *trec = reinterpret_cast<psy::TileRec *>(reinterpret_cast<uint8_t *>(tiles) + 8ull * pw.e_tcap);
+    auto *spans =
+        reinterpret_cast<uint64_t *>(reinterpret_cast<uint8_t *>(trec) + sizeof(psy::TileRec) * pw.e_tcap);
+    auto *shist = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(spans) + 8ull * (pw.e_tcap / psy::kSpanTiles));
     HIPCHK(hipMemsetAsync(cnt, 0, 64, s));
-    psy::PlanArgs p{a.in_off, n, cnt64, slist, mlist, tiles, spans, lmeta, lmax, tcap, kSmallMax,
-                    capturing ? ~0ull : c->large_min};
+    psy::PlanArgs p{a.in_off, n, cnt64, slist, mlist, tiles, spans, lmeta, lcap, tcap, kSmallMax, c->large_min,
+                    small_on ? 1u : 0u};
     const uint32_t per = psy::kPlanThreads * psy::kPlanPer;
     hipLaunchKernelGGL(psy::tdt_encode_plan_kernel, dim3((uint32_t)(((uint64_t)n + per - 1) / per)),
                        dim3(psy::kPlanThreads), 0, s, p);
     HIPCHK(hipGetLastError());
-    uint32_t ns = n, nm = n, nl = 0, nt = 0, nsp = 0;
-    if (!capturing) {
-        HIPCHK(hipMemcpyAsync(pw.host, cnt, 64, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
-        const uint64_t *h = reinterpret_cast<const uint64_t *>(pw.host);
-        ns = (uint32_t)h[0];
-        nm = (uint32_t)h[1];
-        nl = (uint32_t)std::min<uint64_t>(h[2], lmax);
-        nt = (uint32_t)std::min<uint64_t>(h[3], tcap);
-        nsp = (uint32_t)std::min<uint64_t>(h[4], tcap / psy::kSpanTiles);
-    }
-    // large messages: span histograms, mapping, tile counts, scan, emit
+    if (!capturing && (st = record_counts(H, cnt, s))) return st;
+    a.pcnt = cnt;
+    const uint32_t ovf512 = (uint32_t)c->cus * 3, ovf64 = (uint32_t)c->cus * 24;
+    // main launch over [0, g) + overflow launch over [g, count) of one class
+    auto both = [&](uint32_t g, uint32_t bound, uint32_t ovf, auto &&main, auto &&over) {
+        if (g) main(0u, g);
+        if (g < bound) over(g, std::min(ovf, bound - g));
+    };
     bool forked = false;
-    if (nt) {
-        const int fr = fork_side(pw, s);
+    hipStream_t ts = s;  // the tile pipeline's (and the small list's) stream
+    if (tiles_on) {
+        const int fr = c->no_side ? -1 : fork_side(pw, s);
         if (fr > 0) return fr;
         forked = fr == TDT_OK;
-        hipStream_t s0 = s;
-        if (forked) s = pw.side;
+        if (forked) ts = pw.side;
         a.tiles = tiles;
-        a.tile_count = cnt + 6;
-        a.tile_cap = tcap;
         a.spans = spans;
         a.lmeta = lmeta;
         a.trec = trec;
         a.shist = shist;
-        a.list_base = 0;
-        hipLaunchKernelGGL((psy::tdt_encode_kernel<WS, 512, 8, psy::MODE_ENCODE, 0, 1>), dim3(nsp), dim3(512), 0, s, a);
-        hipLaunchKernelGGL((psy::tdt_encode_kernel<WS, 512, 8, psy::MODE_ENCODE, 0, 4>), dim3(nl), dim3(512), 0, s, a);
-        hipLaunchKernelGGL((psy::tdt_encode_kernel<WS, 512, 8, psy::MODE_ENCODE, 0, 2>), dim3(nt), dim3(512), 0, s, a);
-        hipLaunchKernelGGL((psy::tdt_encode_lscan_kernel<WS>), dim3(nl), dim3(64), 0, s, a, cnt + 4, lmax);
-        hipLaunchKernelGGL((psy::tdt_encode_kernel<WS, 512, 8, psy::MODE_ENCODE, 0, 3>), dim3(nt), dim3(512), 0, s, a);
-        s = s0;
+        a.lcap = lcap;
+        a.tcap = tcap;
+#define PSY_TILE_STEP(TL, IDX, BOUND)                                                                           \
+        both(guess(H, IDX, BOUND, 0), BOUND, ovf512,                                                            \
+             [&](uint32_t b, uint32_t g) {                                                                      \
+                 a.list_base = b;                                                                               \
+                 hipLaunchKernelGGL((psy::tdt_encode_kernel<WS, 512, 8, MODE_ENCODE, 0, TL, 0>), dim3(g), dim3(512), \
+                                    0, ts, a);                                                                  \
+             },                                                                                                 \
+             [&](uint32_t b, uint32_t g) {                                                                      \
+                 a.list_base = b;                                                                               \
+                 hipLaunchKernelGGL((psy::tdt_encode_kernel<WS, 512, 8, MODE_ENCODE, 0, TL, 1>), dim3(g), dim3(512), \
+                                    0, ts, a);                                                                  \
+             })
+        PSY_TILE_STEP(1, 8, scap);  // span histograms
+        PSY_TILE_STEP(4, 4, lcap);  // mapping per large message
+        PSY_TILE_STEP(2, 6, tcap);  // per-tile counts
+        hipLaunchKernelGGL((psy::tdt_encode_lscan_kernel<WS>), dim3(std::max(1u, std::min(lcap, 1024u))), dim3(64), 0,
+                           ts, a, cnt + 4, lcap);
+        PSY_TILE_STEP(3, 6, tcap);  // emit
+#undef PSY_TILE_STEP
     }
-    // medium, then small messages: one workgroup per list entry
+    // medium messages: one workgroup per list entry
     a.list = mlist;
     a.list_count = cnt + 2;
-    launch_list(nm, 512, [&](uint32_t b, uint32_t g) {
-        a.list_base = b;
-        hipLaunchKernelGGL((psy::tdt_encode_kernel<WS, 512, 8, psy::MODE_ENCODE, 0, 0>), dim3(g), dim3(512), 0, s, a);
-    });
+    both(guess(H, 2, n, n), n, ovf512,
+         [&](uint32_t b, uint32_t g) {
+             launch_list(g, 512, [&](uint32_t b2, uint32_t g2) {
+                 a.list_base = b + b2;
+                 hipLaunchKernelGGL((psy::tdt_encode_kernel<WS, 512, 8, MODE_ENCODE, 0, 0, 0>), dim3(g2), dim3(512),
+                                    0, s, a);
+             });
+         },
+         [&](uint32_t b, uint32_t g) {
+             a.list_base = b;
+             hipLaunchKernelGGL((psy::tdt_encode_kernel<WS, 512, 8, MODE_ENCODE, 0, 0, 1>), dim3(g), dim3(512), 0, s,
+                                a);
+         });
     // small messages behind the tile pipeline on the side stream (the two streams' loads balance
     // better: C4's tile pipeline is shorter than its medium list)
-    const hipStream_t ss = forked && !std::getenv("PSYNE_TDT_SMALL_MAIN") ? pw.side : s;
-    a.list = slist;
-    a.list_count = cnt;
-    launch_list(ns, 64, [&](uint32_t b, uint32_t g) {
-        a.list_base = b;
-        hipLaunchKernelGGL((psy::tdt_encode_kernel<WS, 64, 4, psy::MODE_ENCODE, 0, 0>), dim3(g), dim3(64), 0, ss, a);
-    });
+    if (small_on) {
+        const hipStream_t ss = forked && !c->small_main ? pw.side : s;
+        a.list = slist;
+        a.list_count = cnt;
+        both(guess(H, 0, n, n), n, ovf64,
+             [&](uint32_t b, uint32_t g) {
+                 launch_list(g, 64, [&](uint32_t b2, uint32_t g2) {
+                     a.list_base = b + b2;
+                     hipLaunchKernelGGL((psy::tdt_encode_kernel<WS, 64, 4, MODE_ENCODE, 0, 0, 0>), dim3(g2), dim3(64),
+                                        0, ss, a);
+                 });
+             },
+             [&](uint32_t b, uint32_t g) {
+                 a.list_base = b;
+                 hipLaunchKernelGGL((psy::tdt_encode_kernel<WS, 64, 4, MODE_ENCODE, 0, 0, 1>), dim3(g), dim3(64), 0,
+                                    ss, a);
+             });
+    }
     if (forked) return join_side(pw, s);
     return TDT_OK;
 }
@@ -362,7 +508,7 @@ int prep(tdt_ctx *c, uint32_t n_msgs, hipStream_t s, uint8_t *&wsp, bool lookbac
     HIPCHK(hipSetDevice(c->device));
     if (!wsp) {
         const bool fresh = c->ws == nullptr;
-        int st = ensure_ws(c, lookback ? n_msgs : 0);
+        int st = ensure_ws(c, lookback ? n_msgs : 0, s);
         if (st) return st;
         wsp = c->ws;
         if (!lookback) {
@@ -424,78 +570,122 @@ int encode_common(tdt_ctx *c, int mode, const uint8_t *d_in, const uint64_t *d_i
     return TDT_OK;
 }
 
-// Slotted decode: a plan kernel separates the large blobs (decoded size > large_min) from the
-// rest; the rest decode one wave each; the large ones through the prep / block / scan / tile
-// passes (tdt_decode.h).  Grids are sized from the plan's counts (read back; conservative
-// under stream capture, where every blob takes the one-wave path).
-constexpr uint32_t kDLmax = 1u << 16, kDBcap = 1u << 23, kDTcap = 1u << 20;
+// Slotted decode: a plan kernel separates the large blobs (decoded size > large_min and
+// > 1/4096 of the batch) and the blobs decoding to <= 1 KiB from the rest; the rest decode one
+// wave each, the small ones one wave each with one-round windows, the large ones through the
+// prep / block / scan / tile passes (tdt_decode.h).  As for encode, the list lengths stay on
+// the device: main grids from an earlier call's counts, overflow launches past them.
+constexpr uint32_t kDLmax = 1u << 16, kDBcap = 1u << 23, kDTcap = 1u << 20;  // full budgets
+constexpr uint32_t kDL0 = 1024, kDB0 = 1u << 16, kDT0 = 8192;                 // starting budgets
 constexpr uint64_t kDSmallMax = 1024;  // decoded sizes up to one window of one round
-size_t dlarge_bytes() {
-    return (size_t)kDLmax * sizeof(psy::DMeta) + 8ull * kDBcap + 4ull * kDTcap + 8ull * kDTcap;
+size_t dlarge_bytes(uint32_t lcap, uint32_t bcap, uint32_t tcap) {
+    return (size_t)lcap * sizeof(psy::DMeta) + 8ull * bcap + 4ull * tcap + 8ull * tcap;
+}
+
+int ensure_dlarge(PlanWS &w, hipStream_t s) {
+    uint32_t lc = w.d_lcap ? w.d_lcap : kDL0, bc = w.d_bcap ? w.d_bcap : kDB0, tc = w.d_tcap ? w.d_tcap : kDT0;
+    if (w.dh.valid) {
+        lc = std::max(lc, pow2_at_least(w.dh.v[2], kDL0, kDLmax));
+        tc = std::max(tc, pow2_at_least(w.dh.v[4], kDT0, kDTcap));
+        bc = std::max(bc, pow2_at_least(w.dh.v[6], kDB0, kDBcap));
+    }
+    if (w.dlarge && lc == w.d_lcap && bc == w.d_bcap && tc == w.d_tcap) return TDT_OK;
+    if (w.dlarge) {
+        int st = drain(w, s);
+        if (st) return st;
+        HIPCHK(hipFree(w.dlarge));
+        w.dlarge = nullptr;
+        w.d_lcap = w.d_bcap = w.d_tcap = 0;
+    }
+    HIPCHK(hipMalloc(&w.dlarge, dlarge_bytes(lc, bc, tc)));
+    w.d_lcap = lc;
+    w.d_bcap = bc;
+    w.d_tcap = tc;
+    return TDT_OK;
 }
 
 int launch_decode_slotted(tdt_ctx *c, PlanWS &pw, psy::DecodeArgs a, hipStream_t s) {
     const uint32_t n = a.n_msgs;
-    int st = ensure_plan(pw, n);
+    int st = ensure_plan(pw, n, s);
     if (st) return st;
-    if (!pw.dlarge) HIPCHK(hipMalloc(&pw.dlarge, dlarge_bytes()));
+    const bool capturing = ::capturing(s);
+    CountHist &H = pw.dh;
+    if (!capturing) H.refresh();
+    const bool small_on = !H.valid || H.v[10] > 0;  // counter 5: small blobs, listed or not
+    bool large_on = !H.valid || H.v[2] > 0;
+    if (large_on && !capturing) {
+        st = ensure_dlarge(pw, s);
+        if (st) return st;
+    }
+    large_on = large_on && pw.dlarge;
     auto *cnt = reinterpret_cast<unsigned long long *>(pw.buf);
+    auto *cnt32 = reinterpret_cast<uint32_t *>(pw.buf);
     auto *list = reinterpret_cast<uint32_t *>(pw.buf + 256);
-    auto *dmeta = reinterpret_cast<psy::DMeta *>(pw.dlarge);
-    auto *bent = reinterpret_cast<uint32_t *>(pw.dlarge + (size_t)kDLmax * sizeof(psy::DMeta));
-    uint32_t *bsum = bent + kDBcap, *tent = bsum + kDBcap, *tblk = tent + kDTcap;
-    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-    HIPCHK(hipStreamIsCapturing(s, &cap));
-    const bool capturing = cap != hipStreamCaptureStatusNone;
-    HIPCHK(hipMemsetAsync(cnt, 0, 40, s));
     uint32_t *slist = list + n;
-    // (under stream capture the counts cannot be read back: every blob then takes the one list)
-    psy::DPlanArgs p{a.in, a.in_off, a.in_len, n, cnt, list, slist, capturing ? 0 : kDSmallMax, dmeta, bent, tent,
-                     kDLmax, kDBcap, kDTcap, capturing ? ~0ull : c->large_min};
+    const uint32_t lcap = large_on ? pw.d_lcap : 0u, bcap = large_on ? pw.d_bcap : 0u,
+                   tcap = large_on ? pw.d_tcap : 0u;
+    auto *dmeta = reinterpret_cast<psy::DMeta *>(pw.dlarge);
+    auto *bent = reinterpret_cast<uint32_t *>(pw.dlarge + (size_t)pw.d_lcap * sizeof(psy::DMeta));
+    uint32_t *bsum = bent + pw.d_bcap, *tent = bsum + pw.d_bcap, *tblk = tent + pw.d_tcap;
+    HIPCHK(hipMemsetAsync(cnt, 0, 64, s));
+    psy::DPlanArgs p{a.in, a.in_off, a.in_len, n, cnt, list, slist, kDSmallMax, dmeta, bent, tent,
+                     lcap, bcap, tcap, c->large_min, small_on ? 1u : 0u};
     hipLaunchKernelGGL(psy::tdt_decode_plan_kernel, dim3((uint32_t)(((uint64_t)n + 4095) / 4096)), dim3(1024), 0, s, p);
     HIPCHK(hipGetLastError());
-    uint32_t nn = n, nl = 0, nb = 0, nt = 0, ns = 0;
-    if (!capturing) {
-        HIPCHK(hipMemcpyAsync(pw.host, cnt, 40, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
-        const uint64_t *h = reinterpret_cast<const uint64_t *>(pw.host);
-        nn = (uint32_t)h[0];
-        nl = (uint32_t)std::min<uint64_t>(h[1], kDLmax);
-        nt = (uint32_t)std::min<uint64_t>(h[2], kDTcap);
-        nb = (uint32_t)std::min<uint64_t>(h[3], kDBcap);
-        ns = (uint32_t)h[4];
-    }
-    a.list = list;
+    if (!capturing && (st = record_counts(H, cnt, s))) return st;
     a.dmeta = dmeta;
     a.bent = bent;
     a.bsum = bsum;
     a.tent = tent;
     a.tblk = tblk;
+    a.pcnt = cnt32;
+    a.lcap = lcap;
+    a.bcap = bcap;
+    a.tcap = tcap;
+    const uint32_t ovf = (uint32_t)c->cus * 32;
+    // one-wave list kernels: main launch over [0, g), overflow launch over [g, count)
+    auto lists = [&](uint32_t g, hipStream_t ls, auto main_k, auto over_k) {
+        if (g) launch_list(g, 64, [&](uint32_t b, uint32_t k) {
+            a.list_base = b;
+            hipLaunchKernelGGL(main_k, dim3(k), dim3(64), 0, ls, a);
+        });
+        if (g < n) {
+            a.list_base = g;
+            hipLaunchKernelGGL(over_k, dim3(std::min(ovf, n - g)), dim3(64), 0, ls, a);
+        }
+    };
     bool forked = false;
-    if (nl) {
-        const int fr = fork_side(pw, s);
+    hipStream_t ts = s;
+    if (large_on) {
+        const int fr = c->no_side ? -1 : fork_side(pw, s);
         if (fr > 0) return fr;
         forked = fr == TDT_OK;
-        hipStream_t s0 = s;
-        if (forked) s = pw.side;
-        hipLaunchKernelGGL(psy::tdt_decode_lprep_kernel, dim3(nl), dim3(256), 0, s, a);
-        if (nb) hipLaunchKernelGGL(psy::tdt_decode_lblock_kernel, dim3((nb + 3) / 4), dim3(256), 0, s, a, nb);
-        hipLaunchKernelGGL(psy::tdt_decode_lscan_kernel, dim3(nl, 2), dim3(64), 0, s, a);
-        a.list_base = 0;
-        hipLaunchKernelGGL(psy::tdt_decode_ltile_kernel, dim3(nt), dim3(64), 0, s, a);
-        s = s0;
+        if (forked) ts = pw.side;
+        const uint32_t gl = std::max(1u, std::min(lcap, 1024u));
+        hipLaunchKernelGGL(psy::tdt_decode_lprep_kernel, dim3(gl), dim3(256), 0, ts, a);
+        hipLaunchKernelGGL(psy::tdt_decode_lblock_kernel, dim3(std::max(1u, std::min((bcap + 3) / 4, ovf / 4))),
+                           dim3(256), 0, ts, a);
+        hipLaunchKernelGGL(psy::tdt_decode_lscan_kernel, dim3(gl, 2), dim3(64), 0, ts, a);
+        const uint32_t gt = guess(H, 4, tcap, 0);
+        if (gt) {
+            a.list_base = 0;
+            hipLaunchKernelGGL(psy::tdt_decode_ltile_kernel<0>, dim3(gt), dim3(64), 0, ts, a);
+        }
+        if (gt < tcap) {
+            a.list_base = gt;
+            hipLaunchKernelGGL(psy::tdt_decode_ltile_kernel<1>, dim3(std::min(ovf, tcap - gt)), dim3(64), 0, ts, a);
+        }
     }
-    launch_list(nn, 64, [&](uint32_t b, uint32_t g) {
-        a.list_base = b;
-        hipLaunchKernelGGL((psy::tdt_decode_kernel<0>), dim3(g), dim3(64), 0, s, a);
-    });
+    a.list = list;
+    a.list_count = cnt32;
+    lists(guess(H, 0, n, n), s, psy::tdt_decode_kernel<0, psy::kDecWR, 0>, psy::tdt_decode_kernel<0, psy::kDecWR, 1>);
     // small blobs: one-round windows (a third less LDS per wave: more blobs in flight per CU)
-    const hipStream_t ss = forked && !std::getenv("PSYNE_TDT_SMALL_MAIN") ? pw.side : s;
-    a.list = slist;
-    launch_list(ns, 64, [&](uint32_t b, uint32_t g) {
-        a.list_base = b;
-        hipLaunchKernelGGL((psy::tdt_decode_kernel<0, 1>), dim3(g), dim3(64), 0, ss, a);
-    });
+    if (small_on) {
+        a.list = slist;
+        a.list_count = cnt32 + 8;
+        lists(guess(H, 8, n, n), forked && !c->small_main ? pw.side : s, psy::tdt_decode_kernel<0, 1, 0>,
+              psy::tdt_decode_kernel<0, 1, 1>);
+    }
     if (forked) return join_side(pw, s);
     return TDT_OK;
 }
@@ -558,15 +748,27 @@ int ensure_host_dev(tdt_ctx *c, size_t bytes) {
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 // ---------------------------------------------------------------------------------------
-// Host pipeline (the TCP socket-buffer case).  The batch is cut into chunks of whole
-// messages (<= kHostChunk input bytes); chunk c runs on slot c % 2 — its own stream, device
-// buffer and look-back workspace — as H2D(input, offsets) → batch kernel → D2H.  While the
-// host waits for chunk c's output size (encode: the compacted size is only known after the
-// kernel), chunk c + 1's copies and kernel are already queued on the other stream, so PCIe
-// transfers in both directions overlap the kernels.
-constexpr uint64_t kHostChunk = 256ull << 20;
+// Host pipeline (the TCP socket-buffer case: SimpleTCP sends from and receives into host
+// memory, tcp_simple.hpp:68-91, :153-194).  The batch is cut into chunks of whole messages
+// (<= kHostChunk input bytes); chunk c runs on slot c % 2 — its own stream, device buffer,
+// look-back workspace and pinned buffers — as H2D → batch kernel → D2H, and the host finishes
+// chunk c - 1 (its output) while chunk c is on the GPU.  Caller buffers that are not pinned
+// (std::vector socket buffers, numpy arrays) are staged through the slot's pinned buffers by a
+// pool of host threads (parallel memcpy: one thread's memcpy is far below the PCIe rate);
+// pinned caller buffers are DMA'd directly.  Every device → host copy lands in pinned memory,
+// so no copy blocks the host behind the kernels.
+constexpr uint64_t kHostChunk = 64ull << 20;
 
-int ensure_slot(tdt_ctx *c, int k, size_t dev_bytes, size_t pin_words) {
+bool is_pinned(const void *p) {
+    hipPointerAttribute_t at{};
+    if (!p || hipPointerGetAttributes(&at, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return at.type == hipMemoryTypeHost;
+}
+
+int ensure_slot(tdt_ctx *c, int k, size_t dev_bytes, size_t pin_words, size_t sin, size_t sout) {
     auto &h = c->hs[k];
     if (!h.stream) {
         HIPCHK(hipStreamCreateWithFlags(&h.stream, hipStreamNonBlocking));
@@ -581,13 +783,23 @@ int ensure_slot(tdt_ctx *c, int k, size_t dev_bytes, size_t pin_words) {
         HIPCHK(hipMalloc(&h.dev, dev_bytes));
         h.dev_bytes = dev_bytes;
     }
-    if (pin_words > h.pin_words) {
-        if (h.pin) HIPCHK(hipHostFree(h.pin));
-        h.pin = nullptr;
-        h.pin_words = 0;
-        HIPCHK(hipHostMalloc(&h.pin, 8 * pin_words, hipHostMallocDefault));
-        h.pin_words = pin_words;
-    }
+    auto pinned = [](uint8_t *&buf, size_t &have, size_t need) -> int {
+        if (need <= have) return TDT_OK;
+        if (buf) HIPCHK(hipHostFree(buf));
+        buf = nullptr;
+        have = 0;
+        const size_t cap = std::max(need, have * 2);
+        HIPCHK(hipHostMalloc(&buf, cap, hipHostMallocDefault));
+        have = cap;
+        return TDT_OK;
+    };
+    uint8_t *pw = reinterpret_cast<uint8_t *>(h.pin);
+    size_t pb = 8 * h.pin_words;
+    int st = pinned(pw, pb, 8 * pin_words);
+    if (st) return st;
+    h.pin = reinterpret_cast<uint64_t *>(pw);
+    h.pin_words = pb / 8;
+    if ((st = pinned(h.stage_in, h.sin_bytes, sin)) || (st = pinned(h.stage_out, h.sout_bytes, sout))) return st;
     return TDT_OK;
 }
 
@@ -603,7 +815,7 @@ int sync_slot(tdt_ctx *c, tdt_ctx::HostSlot &h) {
 
 struct Chunk {
     uint32_t m0 = 0, n = 0;
-    uint64_t in_bytes = 0, cap = 0;
+    uint64_t in_bytes = 0, cap = 0, base = 0;
     size_t o_off = 0, o_out = 0, o_ooff = 0, o_st = 0, o_ws = 0;
 };
 
@@ -631,6 +843,8 @@ Chunk plan_chunk(const uint64_t *h_in_off, uint32_t m0, uint32_t n_msgs, bool en
 }
 
 size_t chunk_dev_bytes(const Chunk &k) { return k.o_ws + kCounterBytes + 8ull * (k.n + 1); }
+// pinned words of a slot: in_off (n+1) | out_off or slots (n+1) | lengths (n) | status (n int32)
+size_t chunk_pin_words(const Chunk &k) { return 3ull * k.n + 2 + (k.n + 1) / 2; }
 
 // decode: the decoded size of every blob from its header (the kernel validates; a blob it
 // rejects gets 0 and its bytes are dropped when the output is compacted)
@@ -648,6 +862,7 @@ uint64_t host_decoded_size(const uint8_t *b, uint64_t len) {
 int host_encode(tdt_ctx *c, const uint8_t *h_in, const uint64_t *h_in_off, uint32_t n_msgs, uint8_t *h_out,
                 uint64_t out_cap, uint64_t *h_out_off, int32_t *h_status) {
     const int ws = c->cfg.word_size;
+    const bool pin_in = is_pinned(h_in + h_in_off[0]), pin_out = is_pinned(h_out);
     std::vector<Chunk> ch;
     for (uint32_t m = 0; m < n_msgs;) {
         ch.push_back(plan_chunk(h_in_off, m, n_msgs, true, ws, nullptr));
@@ -658,39 +873,53 @@ int host_encode(tdt_ctx *c, const uint8_t *h_in, const uint64_t *h_in_off, uint3
     auto issue = [&](size_t ci) -> int {
         const Chunk &k = ch[ci];
         auto &h = c->hs[ci & 1];
-        int st = ensure_slot(c, (int)(ci & 1), chunk_dev_bytes(k), 2ull * (k.n + 1));
+        int st = ensure_slot(c, (int)(ci & 1), chunk_dev_bytes(k), chunk_pin_words(k), pin_in ? 0 : k.in_bytes,
+                             pin_out ? 0 : k.cap);
         if (st) return st;
         st = sync_slot(c, h);  // the slot's previous chunk is done with its buffers
         if (st) return st;
-        uint64_t *pin_in = h.pin;
+        uint64_t *pin_in_off = h.pin;
         const uint64_t b0 = h_in_off[k.m0];
-        for (uint32_t i = 0; i <= k.n; ++i) pin_in[i] = h_in_off[k.m0 + i] - b0;
+        for (uint32_t i = 0; i <= k.n; ++i) pin_in_off[i] = h_in_off[k.m0 + i] - b0;
+        const uint8_t *src = h_in + b0;
+        if (!pin_in) {
+            c->pool->copy(h.stage_in, src, k.in_bytes);
+            src = h.stage_in;
+        }
         uint8_t *d = h.dev;
         auto *doff = reinterpret_cast<uint64_t *>(d + k.o_off);
         auto *dooff = reinterpret_cast<uint64_t *>(d + k.o_ooff);
         auto *dst = reinterpret_cast<int32_t *>(d + k.o_st);
-        HIPCHK(hipMemcpyAsync(d, h_in + b0, k.in_bytes, hipMemcpyHostToDevice, h.stream));
-        HIPCHK(hipMemcpyAsync(doff, pin_in, 8ull * (k.n + 1), hipMemcpyHostToDevice, h.stream));
+        HIPCHK(hipMemcpyAsync(d, src, k.in_bytes, hipMemcpyHostToDevice, h.stream));
+        HIPCHK(hipMemcpyAsync(doff, pin_in_off, 8ull * (k.n + 1), hipMemcpyHostToDevice, h.stream));
         st = encode_common(c, psy::MODE_ENCODE, d, doff, k.n, nullptr, d + k.o_out, k.cap, dooff, dst, nullptr, nullptr,
                            nullptr, h.stream, nullptr, nullptr, d + k.o_ws);
         if (st) return st;
         HIPCHK(hipMemcpyAsync(h.flag, d + k.o_ws + 4, 4, hipMemcpyDeviceToHost, h.stream));
         HIPCHK(hipMemcpyAsync(h.pin + (k.n + 1), dooff, 8ull * (k.n + 1), hipMemcpyDeviceToHost, h.stream));
-        if (h_status) HIPCHK(hipMemcpyAsync(h_status + k.m0, dst, 4ull * k.n, hipMemcpyDeviceToHost, h.stream));
+        HIPCHK(hipMemcpyAsync(h.pin + 3ull * k.n + 2, dst, 4ull * k.n, hipMemcpyDeviceToHost, h.stream));
         HIPCHK(hipEventRecord(h.ev, h.stream));
         return TDT_OK;
     };
-    // chunk ci's compacted size is known once its event fires; then queue its data D2H
+    // chunk ci's compacted size is known once its event fires; then its output comes back
     auto finish = [&](size_t ci) -> int {
         const Chunk &k = ch[ci];
         auto &h = c->hs[ci & 1];
         HIPCHK(hipEventSynchronize(h.ev));
-        const uint64_t *pin_out = h.pin + (k.n + 1);
-        const uint64_t total = pin_out[k.n];
+        const uint64_t *pin_out_off = h.pin + (k.n + 1);
+        const uint64_t total = pin_out_off[k.n];
         if (capacity || base + total > out_cap) capacity = true;
-        for (uint32_t i = 0; i < k.n; ++i) h_out_off[k.m0 + i] = base + (capacity ? 0 : pin_out[i]);
-        if (!capacity && total)
-            HIPCHK(hipMemcpyAsync(h_out + base, h.dev + k.o_out, total, hipMemcpyDeviceToHost, h.stream));
+        for (uint32_t i = 0; i < k.n; ++i) h_out_off[k.m0 + i] = base + (capacity ? 0 : pin_out_off[i]);
+        if (h_status) std::memcpy(h_status + k.m0, h.pin + 3ull * k.n + 2, 4ull * k.n);
+        if (!capacity && total) {
+            if (pin_out) {
+                HIPCHK(hipMemcpyAsync(h_out + base, h.dev + k.o_out, total, hipMemcpyDeviceToHost, h.stream));
+            } else {
+                HIPCHK(hipMemcpyAsync(h.stage_out, h.dev + k.o_out, total, hipMemcpyDeviceToHost, h.stream));
+                HIPCHK(hipStreamSynchronize(h.stream));
+                c->pool->copy(h_out + base, h.stage_out, total);
+            }
+        }
         if (!capacity) base += total;
         return TDT_OK;
     };
@@ -711,7 +940,7 @@ int host_encode(tdt_ctx *c, const uint8_t *h_in, const uint64_t *h_in_off, uint3
 int host_decode(tdt_ctx *c, const uint8_t *h_in, const uint64_t *h_in_off, uint32_t n_msgs, uint8_t *h_out,
                 uint64_t out_cap, uint64_t *h_out_off, int32_t *h_status) {
     // decoded sizes from the headers → every chunk's output offsets are known up front: the
-    // decode is slotted at those offsets and every copy is queued without waiting
+    // decode is slotted at those offsets
     std::vector<uint64_t> dsz(n_msgs);
     uint64_t need = 0;
     for (uint32_t i = 0; i < n_msgs; ++i) {
@@ -719,48 +948,76 @@ int host_decode(tdt_ctx *c, const uint8_t *h_in, const uint64_t *h_in_off, uint3
         need += dsz[i];
     }
     if (need > out_cap) return set_err(TDT_E_CAPACITY, "host output capacity exceeded");
+    const bool pin_in = is_pinned(h_in + h_in_off[0]), pin_out = is_pinned(h_out);
     std::vector<Chunk> ch;
+    uint64_t base = 0;
     for (uint32_t m = 0; m < n_msgs;) {
         ch.push_back(plan_chunk(h_in_off, m, n_msgs, false, c->cfg.word_size, dsz.data()));
+        ch.back().base = base;
+        base += ch.back().cap;
         m += ch.back().n;
     }
     std::vector<uint64_t> lens(n_msgs);
     std::vector<int32_t> stv(n_msgs);
-    uint64_t base = 0;
-    for (size_t ci = 0; ci < ch.size(); ++ci) {
+    auto issue = [&](size_t ci) -> int {
         const Chunk &k = ch[ci];
         auto &h = c->hs[ci & 1];
-        int st = ensure_slot(c, (int)(ci & 1), chunk_dev_bytes(k) + 8ull * k.n, 2ull * (k.n + 1));
+        int st = ensure_slot(c, (int)(ci & 1), chunk_dev_bytes(k) + 8ull * k.n, chunk_pin_words(k),
+                             pin_in ? 0 : k.in_bytes, pin_out ? 0 : k.cap);
         if (st) return st;
         st = sync_slot(c, h);
         if (st) return st;
-        uint64_t *pin_in = h.pin, *pin_slot = h.pin + (k.n + 1);
+        uint64_t *pin_in_off = h.pin, *pin_slot = h.pin + (k.n + 1);
         const uint64_t b0 = h_in_off[k.m0];
         uint64_t acc = 0;
         for (uint32_t i = 0; i <= k.n; ++i) {
-            pin_in[i] = h_in_off[k.m0 + i] - b0;
+            pin_in_off[i] = h_in_off[k.m0 + i] - b0;
             pin_slot[i] = acc;
             if (i < k.n) acc += dsz[k.m0 + i];
+        }
+        const uint8_t *src = h_in + b0;
+        if (!pin_in) {
+            c->pool->copy(h.stage_in, src, k.in_bytes);
+            src = h.stage_in;
         }
         uint8_t *d = h.dev;
         auto *doff = reinterpret_cast<uint64_t *>(d + k.o_off);
         auto *dslot = reinterpret_cast<uint64_t *>(d + k.o_ooff);
         auto *dst = reinterpret_cast<int32_t *>(d + k.o_st);
         auto *dlen = reinterpret_cast<uint64_t *>(d + chunk_dev_bytes(k));
-        HIPCHK(hipMemcpyAsync(d, h_in + b0, k.in_bytes, hipMemcpyHostToDevice, h.stream));
-        HIPCHK(hipMemcpyAsync(doff, pin_in, 8ull * (k.n + 1), hipMemcpyHostToDevice, h.stream));
+        HIPCHK(hipMemcpyAsync(d, src, k.in_bytes, hipMemcpyHostToDevice, h.stream));
+        HIPCHK(hipMemcpyAsync(doff, pin_in_off, 8ull * (k.n + 1), hipMemcpyHostToDevice, h.stream));
         HIPCHK(hipMemcpyAsync(dslot, pin_slot, 8ull * (k.n + 1), hipMemcpyHostToDevice, h.stream));
         st = decode_common(c, false, d, doff, k.n, d + k.o_out, 0, nullptr, nullptr, dst, h.stream, dslot, dlen,
                            nullptr, d + k.o_ws, &h.pw);
         if (st) return st;
         HIPCHK(hipMemcpyAsync(h.flag, d + k.o_ws + 4, 4, hipMemcpyDeviceToHost, h.stream));
-        if (acc) HIPCHK(hipMemcpyAsync(h_out + base, d + k.o_out, acc, hipMemcpyDeviceToHost, h.stream));
-        HIPCHK(hipMemcpyAsync(lens.data() + k.m0, dlen, 8ull * k.n, hipMemcpyDeviceToHost, h.stream));
-        HIPCHK(hipMemcpyAsync(stv.data() + k.m0, dst, 4ull * k.n, hipMemcpyDeviceToHost, h.stream));
-        base += acc;
+        if (acc)
+            HIPCHK(hipMemcpyAsync(pin_out ? h_out + k.base : h.stage_out, d + k.o_out, acc, hipMemcpyDeviceToHost,
+                                  h.stream));
+        HIPCHK(hipMemcpyAsync(h.pin + 2ull * (k.n + 1), dlen, 8ull * k.n, hipMemcpyDeviceToHost, h.stream));
+        HIPCHK(hipMemcpyAsync(h.pin + 3ull * k.n + 2, dst, 4ull * k.n, hipMemcpyDeviceToHost, h.stream));
+        HIPCHK(hipEventRecord(h.ev, h.stream));
+        return TDT_OK;
+    };
+    auto finish = [&](size_t ci) -> int {
+        const Chunk &k = ch[ci];
+        auto &h = c->hs[ci & 1];
+        HIPCHK(hipEventSynchronize(h.ev));
+        if (!pin_out && k.cap) c->pool->copy(h_out + k.base, h.stage_out, k.cap);
+        std::memcpy(lens.data() + k.m0, h.pin + 2ull * (k.n + 1), 8ull * k.n);
+        std::memcpy(stv.data() + k.m0, h.pin + 3ull * k.n + 2, 4ull * k.n);
+        return TDT_OK;
+    };
+    for (size_t ci = 0; ci < ch.size(); ++ci) {
+        int st = issue(ci);
+        if (!st && ci > 0) st = finish(ci - 1);
+        if (st) return st;
     }
+    int st = finish(ch.size() - 1);
+    if (st) return st;
     for (auto &h : c->hs) {
-        int st = h.stream ? sync_slot(c, h) : TDT_OK;
+        st = h.stream ? sync_slot(c, h) : TDT_OK;
         if (st) return st;
     }
     // offsets; blobs the kernel rejected (status != OK, length 0) leave a gap: compact it
@@ -786,6 +1043,7 @@ int host_path(tdt_ctx *c, bool encode, const uint8_t *h_in, const uint64_t *h_in
     if (!h_in_off || !h_out_off) return set_err(TDT_E_ARG, "null offsets");
     HIPCHK(hipSetDevice(c->device));
     std::lock_guard<std::mutex> lk(c->hmu);  // the pipeline slots belong to the context
+    if (!c->pool) c->pool.reset(new CopyPool(c->copy_threads));
     return encode ? host_encode(c, h_in, h_in_off, n_msgs, h_out, out_cap, h_out_off, h_status)
                   : host_decode(c, h_in, h_in_off, n_msgs, h_out, out_cap, h_out_off, h_status);
 }
@@ -847,10 +1105,9 @@ __global__ __launch_bounds__(256) void cp_gather_kernel(const uint8_t *src, cons
 
 static int scan_sizes(tdt_ctx *ctx, uint64_t *d_off, uint32_t n_msgs, hipStream_t stream);
 // The two-phase compaction reads a few bytes back to choose its path: not under stream capture
-// (the one-pass kernels need no read-back), nor with PSYNE_TDT_NO_TWO_PHASE=1.
-static bool two_phase_ok(void *stream) {
-    const char *e = std::getenv("PSYNE_TDT_NO_TWO_PHASE");
-    if (e && *e == '1') return false;
+// (the one-pass kernels need no read-back), nor with the no-two-phase knob.
+static bool two_phase_ok(const tdt_ctx *ctx, void *stream) {
+    if (ctx->no_two_phase) return false;
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing((hipStream_t)stream, &cap) != hipSuccess) return false;
     return cap == hipStreamCaptureStatusNone;
@@ -880,9 +1137,24 @@ int tdt_ctx_create(int device, const tdt_config *cfg, tdt_ctx **out) {
     tdt_ctx *x = new tdt_ctx();
     x->device = device;
     x->cfg = c;
-    // tuning / test overrides: the tiled-path threshold, and a lower tile budget (fallback tests)
+    // tuning / test overrides, read once here (tdt_ctx_set_option changes them later): the
+    // tiled-path threshold, a lower tile budget (fallback tests), the diagnostic stream knobs
     if (const char *e = std::getenv("PSYNE_TDT_LARGE_MIN")) x->large_min = std::strtoull(e, nullptr, 10);
     if (const char *e = std::getenv("PSYNE_TDT_TILE_CAP")) x->tile_cap = (uint32_t)std::strtoul(e, nullptr, 10);
+    auto flag = [](const char *name) {
+        const char *e = std::getenv(name);
+        return e && *e == '1';
+    };
+    x->no_side = flag("PSYNE_TDT_NO_SIDE");
+    x->small_main = flag("PSYNE_TDT_SMALL_MAIN");
+    x->no_two_phase = flag("PSYNE_TDT_NO_TWO_PHASE");
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
+        x->cus = cus;
+    // staging-copy threads: up to 8, within this process's CPU affinity
+    cpu_set_t cs;
+    CPU_ZERO(&cs);
+    if (sched_getaffinity(0, sizeof(cs), &cs) == 0) x->copy_threads = std::max(1, std::min(8, CPU_COUNT(&cs)));
     *out = x;
     return TDT_OK;
 }
@@ -895,12 +1167,16 @@ void tdt_ctx_destroy(tdt_ctx *ctx) {
     if (ctx->cp_buf) (void)hipFree(ctx->cp_buf);
     if (ctx->cp_idx) (void)hipFree(ctx->cp_idx);
     ctx->pw.release();
+    if (ctx->astream) (void)hipStreamSynchronize(ctx->astream);
     if (ctx->h_dev) (void)hipFree(ctx->h_dev);
+    if (ctx->astream) (void)hipStreamDestroy(ctx->astream);
     for (auto &h : ctx->hs) {
         if (h.stream) (void)hipStreamSynchronize(h.stream);
         if (h.dev) (void)hipFree(h.dev);
         if (h.pin) (void)hipHostFree(h.pin);
         if (h.flag) (void)hipHostFree(h.flag);
+        if (h.stage_in) (void)hipHostFree(h.stage_in);
+        if (h.stage_out) (void)hipHostFree(h.stage_out);
         h.pw.release();
         if (h.ev) (void)hipEventDestroy(h.ev);
         if (h.stream) (void)hipStreamDestroy(h.stream);
@@ -921,6 +1197,25 @@ void tdt_ctx_get_metrics(const tdt_ctx *ctx, double *bandwidth_mbps, double *lat
 }
 
 void tdt_ctx_set_size_hint(tdt_ctx *ctx, uint64_t bytes) { ctx->size_hint.store(bytes); }
+
+int tdt_ctx_set_option(tdt_ctx *ctx, int option, uint64_t value) {
+    if (!ctx) return set_err(TDT_E_ARG, "null context");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    switch (option) {
+        case TDT_OPT_LARGE_MIN: ctx->large_min = value; return TDT_OK;
+        case TDT_OPT_TILE_CAP: ctx->tile_cap = (uint32_t)std::min<uint64_t>(value, 0xffffffffu); return TDT_OK;
+        case TDT_OPT_NO_SIDE_STREAM: ctx->no_side = value != 0; return TDT_OK;
+        case TDT_OPT_SMALL_ON_CALLER_STREAM: ctx->small_main = value != 0; return TDT_OK;
+        case TDT_OPT_NO_TWO_PHASE: ctx->no_two_phase = value != 0; return TDT_OK;
+        case TDT_OPT_COPY_THREADS: {
+            std::lock_guard<std::mutex> hl(ctx->hmu);
+            ctx->copy_threads = (int)std::max<uint64_t>(1, std::min<uint64_t>(value, 64));
+            ctx->pool.reset();
+            return TDT_OK;
+        }
+    }
+    return set_err(TDT_E_ARG, "unknown option");
+}
 
 int tdt_should_transform(const tdt_ctx *ctx, uint64_t n) {
     if (n < ctx->cfg.min_tensor_size) return 0;
@@ -944,7 +1239,7 @@ uint64_t tdt_encode_bound(uint64_t n, int32_t word_size) {
 // slotted (the message-class kernels), then the lengths are scanned and the blobs gathered.
 int tdt_encode_batch(tdt_ctx *ctx, const uint8_t *d_in, const uint64_t *d_in_off, uint32_t n_msgs, uint8_t *d_out,
                      uint64_t out_cap, uint64_t *d_out_off, int32_t *d_status, void *stream) {
-    if (!ctx || n_msgs == 0 || !d_in_off || !d_out || !d_out_off || !two_phase_ok(stream))
+    if (!ctx || n_msgs == 0 || !d_in_off || !d_out || !d_out_off || !two_phase_ok(ctx, stream))
         return encode_common(ctx, psy::MODE_ENCODE, d_in, d_in_off, n_msgs, nullptr, d_out, out_cap, d_out_off,
                              d_status, nullptr, nullptr, nullptr, stream);
     hipStream_t s = (hipStream_t)stream;
@@ -1021,7 +1316,7 @@ int tdt_analyze_batch(tdt_ctx *ctx, const uint8_t *d_in, const uint64_t *d_in_of
 // TDT_E_CAPACITY per blob.
 int tdt_decode_batch(tdt_ctx *ctx, const uint8_t *d_in, const uint64_t *d_in_off, uint32_t n_msgs, uint8_t *d_out,
                      uint64_t out_cap, uint64_t *d_out_off, int32_t *d_status, void *stream) {
-    if (ctx && n_msgs && d_in_off && d_out && d_out_off && two_phase_ok(stream)) {
+    if (ctx && n_msgs && d_in_off && d_out && d_out_off && two_phase_ok(ctx, stream)) {
         hipStream_t s = (hipStream_t)stream;
         HIPCHK(hipSetDevice(ctx->device));
         int st = tdt_decode_slots(ctx, d_in, d_in_off, nullptr, n_msgs, d_out_off, d_status, stream);
@@ -1105,14 +1400,16 @@ int tdt_decode_host(tdt_ctx *ctx, const uint8_t *h_in, const uint64_t *h_in_off,
     return host_path(ctx, false, h_in, h_in_off, n_msgs, h_out, out_cap, h_out_off, h_status);
 }
 
-int tdt_ctx_error_flags(tdt_ctx *ctx, uint32_t *flags) {
+int tdt_ctx_error_flags(tdt_ctx *ctx, void *stream, uint32_t *flags) {
     if (!ctx || !flags) return set_err(TDT_E_ARG, "null argument");
     *flags = ctx->host_flags.load();
     if (!ctx->ws) return TDT_OK;
     HIPCHK(hipSetDevice(ctx->device));
-    HIPCHK(hipDeviceSynchronize());
+    // stream-ordered read of the flag word: waits for the batches issued on `stream` only
     uint32_t f = 0;
-    HIPCHK(hipMemcpy(&f, ctx->ws + 4, 4, hipMemcpyDeviceToHost));
+    hipStream_t s = (hipStream_t)stream;
+    HIPCHK(hipMemcpyAsync(&f, ctx->ws + 4, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
     *flags |= f;
     return TDT_OK;
 }
@@ -1138,16 +1435,20 @@ int tdt_analyze_host(tdt_ctx *ctx, const uint8_t *h_in, const uint64_t *h_in_off
     uint8_t *d = ctx->h_dev;
     std::vector<uint64_t> tmp(n_msgs + 1);
     for (uint32_t i = 0; i <= n_msgs; ++i) tmp[i] = h_in_off[i] - h_in_off[0];
-    HIPCHK(hipMemcpy(d, h_in + h_in_off[0], in_bytes, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(d + o_off, tmp.data(), 8ull * (n_msgs + 1), hipMemcpyHostToDevice));
+    // on the context's own stream (synchronising that stream only, not the device)
+    std::lock_guard<std::mutex> hl(ctx->hmu);
+    if (!ctx->astream) HIPCHK(hipStreamCreateWithFlags(&ctx->astream, hipStreamNonBlocking));
+    hipStream_t s = ctx->astream;
+    HIPCHK(hipMemcpyAsync(d, h_in + h_in_off[0], in_bytes, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(d + o_off, tmp.data(), 8ull * (n_msgs + 1), hipMemcpyHostToDevice, s));
     st = encode_common(ctx, psy::MODE_ANALYZE, d, reinterpret_cast<uint64_t *>(d + o_off), n_msgs, nullptr, nullptr,
                        0, nullptr, reinterpret_cast<int32_t *>(d + o_st), nullptr,
-                       reinterpret_cast<double *>(d + o_ent), reinterpret_cast<int32_t *>(d + o_map), nullptr);
+                       reinterpret_cast<double *>(d + o_ent), reinterpret_cast<int32_t *>(d + o_map), s);
     if (st) return st;
-    HIPCHK(hipDeviceSynchronize());
-    if (h_entropy) HIPCHK(hipMemcpy(h_entropy, d + o_ent, 8ull * n_msgs * ws, hipMemcpyDeviceToHost));
-    if (h_mapping) HIPCHK(hipMemcpy(h_mapping, d + o_map, 4ull * n_msgs * ws, hipMemcpyDeviceToHost));
-    if (h_status) HIPCHK(hipMemcpy(h_status, d + o_st, 4ull * n_msgs, hipMemcpyDeviceToHost));
+    if (h_entropy) HIPCHK(hipMemcpyAsync(h_entropy, d + o_ent, 8ull * n_msgs * ws, hipMemcpyDeviceToHost, s));
+    if (h_mapping) HIPCHK(hipMemcpyAsync(h_mapping, d + o_map, 4ull * n_msgs * ws, hipMemcpyDeviceToHost, s));
+    if (h_status) HIPCHK(hipMemcpyAsync(h_status, d + o_st, 4ull * n_msgs, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
     return TDT_OK;
 }
 
@@ -1165,6 +1466,7 @@ const char *tdt_status_string(int status) {
         case TDT_E_BAD_HEADER: return "TDT: word size 0";
         case TDT_E_CONFIG: return "TDT: invalid configuration";
         case TDT_E_HIP: return "TDT: HIP runtime error";
+        case TDT_E_CAPTURE: return "TDT: workspace growth needed under stream capture";
         case TDT_E_ARG: return "TDT: invalid argument";
     }
     return "TDT: unknown status";
@@ -1187,6 +1489,7 @@ static int scan_sizes(tdt_ctx *ctx, uint64_t *d_slot_off, uint32_t n_msgs, hipSt
     if (nb > 1) {
         std::lock_guard<std::mutex> lk(ctx->mu);
         if (nb > ctx->slot_sums_n) {
+            if (int st = no_growth_in_capture(stream)) return st;
             if (ctx->slot_sums) HIPCHK(hipFree(ctx->slot_sums));
             ctx->slot_sums = nullptr;
             HIPCHK(hipMalloc(&ctx->slot_sums, 8ull * nb));

@@ -1,0 +1,104 @@
+// tdt_copypool.h — host threads for the host pipeline's staging copies (host code only).
+//
+// A pageable caller buffer reaches the GPU through pinned staging: one thread's memcpy moves
+// ~10 GB/s, well below what PCIe takes, so large copies are split over a small pool of
+// threads (the caller's thread takes a share too).  Copies below kParMin run inline.
+#pragma once
+
+#include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <cstddef>
+#include <cstdint>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+class CopyPool {
+  public:
+    explicit CopyPool(int threads) {
+        const int n = std::max(0, threads - 1);  // the caller copies a share itself
+        for (int i = 0; i < n; ++i) th_.emplace_back([this] { work(); });
+    }
+    ~CopyPool() {
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto &t : th_) t.join();
+    }
+    CopyPool(const CopyPool &) = delete;
+    CopyPool &operator=(const CopyPool &) = delete;
+
+    // dst[0, bytes) = src[0, bytes); returns when every part is copied
+    void copy(void *dst, const void *src, size_t bytes) {
+        if (bytes < kParMin || th_.empty()) {
+            std::memcpy(dst, src, bytes);
+            return;
+        }
+        auto job = std::make_shared<Job>();
+        job->d = static_cast<uint8_t *>(dst);
+        job->s = static_cast<const uint8_t *>(src);
+        job->bytes = bytes;
+        job->parts = std::min<size_t>(bytes / kPart + 1, 4 * (th_.size() + 1));
+        job->left.store(job->parts);
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            job_ = job;
+            ++gen_;
+        }
+        cv_.notify_all();
+        run(*job);
+        std::unique_lock<std::mutex> lk(m_);
+        done_.wait(lk, [&] { return job->left.load() == 0; });
+        job_.reset();
+    }
+
+  private:
+    static constexpr size_t kParMin = 1u << 20, kPart = 2u << 20;
+    // one copy call; a worker that wakes late holds a finished job and finds no part left
+    struct Job {
+        uint8_t *d = nullptr;
+        const uint8_t *s = nullptr;
+        size_t bytes = 0, parts = 0;
+        std::atomic<size_t> next{0}, left{0};
+    };
+
+    void run(Job &j) {
+        const size_t per = (j.bytes + j.parts - 1) / j.parts;
+        for (;;) {
+            const size_t i = j.next.fetch_add(1);
+            if (i >= j.parts) return;
+            const size_t b = i * per, e = std::min(j.bytes, b + per);
+            if (b < e) std::memcpy(j.d + b, j.s + b, e - b);
+            if (j.left.fetch_sub(1) == 1) {
+                std::lock_guard<std::mutex> lk(m_);
+                done_.notify_all();
+            }
+        }
+    }
+    void work() {
+        uint64_t seen = 0;
+        for (;;) {
+            std::shared_ptr<Job> j;
+            {
+                std::unique_lock<std::mutex> lk(m_);
+                cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+                if (stop_) return;
+                seen = gen_;
+                j = job_;
+            }
+            if (j) run(*j);
+        }
+    }
+
+    std::vector<std::thread> th_;
+    std::mutex m_;
+    std::condition_variable cv_, done_;
+    bool stop_ = false;
+    uint64_t gen_ = 0;
+    std::shared_ptr<Job> job_;
+};

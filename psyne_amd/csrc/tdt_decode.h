@@ -44,9 +44,14 @@ struct DecodeArgs {
     const uint64_t *slot_off;  // slotted outputs (LB = 0)
     uint64_t *out_len;
     const uint64_t *in_len;  // optional blob lengths (blob i = in[in_off[i] .. +in_len[i]))
-    // slotted batches: blob ids from the plan's list (null: blob id = blockIdx)
+    // slotted batches: blob ids from the plan's list
     const uint32_t *list;
+    const uint32_t *list_count;  // the list's length (device memory: the plan's counter)
     uint32_t list_base;
+    // the plan's counters (u32 view: [2] large blobs, [4] tiles, [6] blocks claimed) and the
+    // budgets it ran with
+    const uint32_t *pcnt;
+    uint32_t lcap, tcap, bcap;
     // large blobs (tiled path)
     DMeta *dmeta;
     const uint32_t *bent;  // block-slot entries (large-blob index)
@@ -990,14 +995,17 @@ struct DPlanArgs {
     const uint64_t *in_off;
     const uint64_t *in_len;
     uint32_t n_msgs;
-    unsigned long long *cnt;  // [0] one-wave blobs, [1] large blobs, [2] tiles, [3] block slots, [4] small blobs
+    // [0] one-wave blobs, [1] large blobs, [2] tiles, [3] block slots, [4] small blobs (listed),
+    // [5] small blobs (listed or not: the host's count history switches the small list back on)
+    unsigned long long *cnt;
     uint32_t *list;
     uint32_t *slist;          // blobs decoding to <= small_max bytes (one-round windows: less LDS per wave)
     uint64_t small_max;
     DMeta *dmeta;
     uint32_t *bent, *tent;
-    uint32_t lmax, bcap, tcap;
+    uint32_t lmax, bcap, tcap;  // (0, 0, 0: no tiled path)
     uint64_t large_min;
+    uint32_t small_on;  // 0: small blobs join the one-wave list
 };
 
 __global__ __launch_bounds__(1024) void tdt_decode_plan_kernel(DPlanArgs p) {
@@ -1010,7 +1018,7 @@ __global__ __launch_bounds__(1024) void tdt_decode_plan_kernel(DPlanArgs p) {
         const uint64_t share = (last - p.in_off[0]) / 4096;
         thr = share > thr ? share : thr;
     }
-    uint64_t isl[4], nt[4], nb[4], j[4], t0[4], b0[4], one[4], pos[4], sm[4], spos[4];
+    uint64_t isl[4], nt[4], nb[4], j[4], t0[4], b0[4], one[4], pos[4], sm[4], spos[4], sc[4], scp[4];
     uint64_t osz_k[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -1062,11 +1070,14 @@ __global__ __launch_bounds__(1024) void tdt_decode_plan_kernel(DPlanArgs p) {
             }
         }
         const bool any = i < p.n_msgs && !large;
-        sm[k] = (any && p.small_max && osz_k[k] <= p.small_max) ? 1u : 0u;
+        const bool small = any && !isl[k] && p.small_max && osz_k[k] <= p.small_max;
+        sc[k] = small ? 1u : 0u;
+        sm[k] = small && p.small_on ? 1u : 0u;
         one[k] = (any && !sm[k]) ? 1u : 0u;
     }
     wg_claim<4>(one, pos, p.cnt, lds);
     wg_claim<4>(sm, spos, p.cnt + 4, lds);
+    wg_claim<4>(sc, scp, p.cnt + 5, lds);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         if (one[k]) p.list[pos[k]] = (blockIdx.x * 4 + k) * 1024 + threadIdx.x;
@@ -1079,10 +1090,12 @@ __global__ __launch_bounds__(1024) void tdt_decode_plan_kernel(DPlanArgs p) {
 __global__ __launch_bounds__(256) void tdt_decode_lprep_kernel(DecodeArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t smem[DecLayout::BYTES];
     __shared__ uint32_t s_tiled, s_fast;
-    const uint32_t j = blockIdx.x;
+    const uint32_t nl = __builtin_amdgcn_readfirstlane(umin(a.pcnt[2], a.lcap));
+    for (uint32_t j = blockIdx.x; j < nl; j += gridDim.x) {  // grid-stride over the large blobs
+    if (j != blockIdx.x) __syncthreads();
     DMeta *m = a.dmeta + j;
     const uint32_t msg = m->msg;
-    if (msg == kNone) return;  // over a budget (the plan emptied its ranges)
+    if (msg == kNone) continue;  // over a budget (the plan emptied its ranges)
     if (threadIdx.x < 64) {
         const int lane = lane_id();
         const uint64_t boff = a.in_off[msg];
@@ -1136,19 +1149,20 @@ __global__ __launch_bounds__(256) void tdt_decode_lprep_kernel(DecodeArgs a) {
     const uint32_t tv = s_tiled ? j : kNone, bv = s_fast ? j : kNone;
     for (uint32_t i = threadIdx.x; i < m->ntiles; i += 256) const_cast<uint32_t *>(a.tent)[m->tile0 + i] = tv;
     for (uint32_t i = threadIdx.x; i < m->nbs; i += 256) const_cast<uint32_t *>(a.bent)[m->blk0 + i] = bv;
+    }
 }
 
 // Block pass: one wave per 512-pair block (8 pairs per lane): the block's count sum.
-__global__ __launch_bounds__(256) void tdt_decode_lblock_kernel(DecodeArgs a, uint32_t nslots) {
-    const uint32_t slot = blockIdx.x * 4u + (threadIdx.x >> 6);
-    if (slot >= nslots) return;
+__global__ __launch_bounds__(256) void tdt_decode_lblock_kernel(DecodeArgs a) {
+    const uint32_t nslots = __builtin_amdgcn_readfirstlane(umin(a.pcnt[6], a.bcap));
+    for (uint32_t slot = blockIdx.x * 4u + (threadIdx.x >> 6); slot < nslots; slot += gridDim.x * 4u) {
     const uint32_t j = a.bent[slot];
-    if (j == kNone) return;
+    if (j == kNone) continue;
     const DMeta *m = a.dmeta + j;
     const uint32_t idx = slot - m->blk0, nb0 = m->nb[0];
     const uint32_t r = idx < nb0 ? 0u : 1u;
     const uint32_t b = r ? idx - nb0 : idx;
-    if (r == 1 && b >= m->nb[1]) return;
+    if (r == 1 && b >= m->nb[1]) continue;
     const uint32_t msg = m->msg;
     const uint64_t boff = a.in_off[msg];
     const uint64_t len = a.in_len ? a.in_len[msg] : a.in_off[msg + 1] - boff;
@@ -1160,14 +1174,17 @@ __global__ __launch_bounds__(256) void tdt_decode_lblock_kernel(DecodeArgs a, ui
     const uint32_t s2 = (pv.x & 0x00ff00ffu) + (pv.y & 0x00ff00ffu) + (pv.z & 0x00ff00ffu) + (pv.w & 0x00ff00ffu);
     const uint32_t tot = wave_reduce<OpAdd>((s2 & 0xffffu) + (s2 >> 16));
     if (lane_id() == 0) a.bsum[m->blk0 + idx] = tot;
+    }
 }
 
 // Scan: one wave per large blob and referenced stream: block sums → block start positions
 // (in place), the stream's decoded length, and each tile's carry block.
 __global__ __launch_bounds__(64) void tdt_decode_lscan_kernel(DecodeArgs a) {
-    DMeta *m = a.dmeta + blockIdx.x;
+    const uint32_t nl = __builtin_amdgcn_readfirstlane(umin(a.pcnt[2], a.lcap));
     const uint32_t r = blockIdx.y;
-    if (m->msg == kNone || !m->tiled || m->H.kind != 2 || (r == 1 && !m->H.two)) return;
+    for (uint32_t j = blockIdx.x; j < nl; j += gridDim.x) {  // grid-stride over the large blobs
+    DMeta *m = a.dmeta + j;
+    if (m->msg == kNone || !m->tiled || m->H.kind != 2 || (r == 1 && !m->H.two)) continue;
     const uint32_t lane = (uint32_t)lane_id();
     const uint32_t n = m->nb[r], base = m->blk0 + (r ? m->nb[0] : 0u);
     const uint64_t TS = (uint64_t)kDecTileGroups * m->H.seg[r];  // stream positions per tile
@@ -1187,12 +1204,12 @@ __global__ __launch_bounds__(64) void tdt_decode_lscan_kernel(DecodeArgs a) {
         run += rdlane(incl, 63);
     }
     if (lane == 0) m->slen[r] = (uint32_t)run;
+    }
 }
 
-// Tile pass: one wave per 32 KiB output tile.
-__global__ __launch_bounds__(64) void tdt_decode_ltile_kernel(DecodeArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t smem[DecLayout::BYTES];
-    const uint32_t slot = a.list_base + blockIdx.x;
+// Tile pass: one wave per 32 KiB output tile (main launch: tiles [list_base, list_base + grid);
+// overflow launch, PS = 1: the tiles past it, grid-stride).
+__device__ __forceinline__ void decode_ltile(const DecodeArgs &a, uint8_t *smem, uint32_t slot) {
     const uint32_t j = a.tent[slot];
     if (j == kNone) return;
     const DMeta *m = a.dmeta + j;
@@ -1234,20 +1251,46 @@ __global__ __launch_bounds__(64) void tdt_decode_ltile_kernel(DecodeArgs a) {
     decode_fast(H, smem, blob, blob + len, dst, ngroups, wbytes, g_lo, g_hi, b0, s0);
 }
 
+template <int PS = 0>
+__global__ __launch_bounds__(64) void tdt_decode_ltile_kernel(DecodeArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t smem[DecLayout::BYTES];
+    const uint32_t nt = __builtin_amdgcn_readfirstlane(umin(a.pcnt[4], a.tcap));
+    const uint32_t i0 = a.list_base + blockIdx.x;
+    if constexpr (PS) {
+        for (uint32_t i = i0; i < nt; i += gridDim.x) {
+            if (i != i0) team_sync<1>();
+            decode_ltile(a, smem, i);
+        }
+    } else {
+        if (i0 < nt) decode_ltile(a, smem, i0);
+    }
+}
+
 // Blob ids: the look-back needs them in dispatch order (atomic ticket); slotted batches take
 // them from the plan's list (or, without one, the workgroup id).
-template <int LB, int WR = kDecWR>
+// List entries are bounded by the plan's device-side count (main launch: one blob per wave over
+// [list_base, list_base + grid); overflow launch, PS = 1: the entries past it, grid-stride).
+template <int LB, int WR = kDecWR, int PS = 0>
 __global__ __launch_bounds__(64, LB ? 6 : 8) void tdt_decode_kernel(DecodeArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t smem[DecLayoutT<WR>::BYTES];
-    uint32_t msg;
     if constexpr (LB) {
         uint32_t t = 0;
         if (lane_id() == 0) t = atomicAdd(a.ticket, 1u);
-        msg = __builtin_amdgcn_readfirstlane(t);
+        decode_one<LB, WR>(a, smem, __builtin_amdgcn_readfirstlane(t));
     } else {
-        msg = a.list ? a.list[a.list_base + blockIdx.x] : a.list_base + blockIdx.x;
+        // (slotted launches always pass the plan's list)
+        const uint32_t cnt = __builtin_amdgcn_readfirstlane(*a.list_count);
+        const uint32_t i0 = a.list_base + blockIdx.x;
+        if constexpr (PS) {
+            for (uint32_t i = i0; i < cnt; i += gridDim.x) {
+                if (i != i0) team_sync<1>();
+                decode_one<LB, WR>(a, smem, a.list[i]);
+            }
+        } else {
+            if (i0 >= cnt) return;
+            decode_one<LB, WR>(a, smem, a.list[i0]);
+        }
     }
-    decode_one<LB, WR>(a, smem, msg);
 }
 
 }  // namespace psy

@@ -102,14 +102,15 @@ struct EncodeArgs {
     uint64_t *out_len;         // slotted outputs: blob lengths
     uint64_t min_tensor;
     int32_t policy_on;  // bandwidth < threshold && cpu <= threshold (host-evaluated atomics)
-    // persistent slotted kernels: message ids from a class list (null: message id = blockIdx)
+    // slotted kernels: message ids from a class list (null: message id = blockIdx)
     const uint32_t *list;
-    const uint32_t *list_count;
+    const uint32_t *list_count;  // the list's length (device memory: the plan's counter)
     uint32_t list_base;  // first list / tile entry of this launch (grids of < 2^32 threads)
-    // tiled large messages: tile / span entries (L index | tile << 32), their counts (capped)
+    // tiled large messages: tile / span entries (L index | tile << 32); the plan's counters
+    // (u32 view: [4] large messages, [6] tiles, [8] spans claimed) and the budgets it ran with
     const uint64_t *tiles;
-    const uint32_t *tile_count;
-    uint32_t tile_cap;
+    const uint32_t *pcnt;
+    uint32_t lcap, tcap;  // large-message entries, tiles (spans: tcap / kSpanTiles)
     const uint64_t *spans;
     LMeta *lmeta;
     TileRec *trec;
@@ -1509,38 +1510,60 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
 
 // Message ids: the compacted API's look-back needs them in dispatch order (atomic ticket);
 // slotted batches take them from a class list (or, without one, the workgroup id); TL > 0:
-// one tile of the batch's tile list per workgroup.  (No persistent loops: around this body a
-// loop makes the compiler keep loop-invariant values live across the whole message and
-// spill at the 80-VGPR budget of 6 waves per SIMD.)
-template <int WS, int TEAM, int G, int MODE, int LB, int TL = 0>
+// one large-message / span / tile entry per workgroup.  List and tile entries are bounded by
+// the plan's device-side counts, so a launch never needs them on the host: the main launch
+// (PS = 0) covers entries [list_base, list_base + grid) with one workgroup each, its grid sized
+// from an earlier plan; the overflow launch (PS = 1) walks the entries past it grid-stride.
+// (Only the overflow instances loop: around this body a loop makes the compiler keep
+// loop-invariant values live across the whole message and spill at the 80-VGPR budget of 6
+// waves per SIMD — correct, but slower.)
+template <int TL>
+__device__ __forceinline__ uint32_t entry_count(const EncodeArgs &a) {
+    uint32_t c;
+    if constexpr (TL == 0) c = *a.list_count;
+    else if constexpr (TL == 4) c = umin(a.pcnt[4], a.lcap);
+    else if constexpr (TL == 1) c = umin(a.pcnt[8], a.tcap / kSpanTiles);
+    else c = umin(a.pcnt[6], a.tcap);
+    return __builtin_amdgcn_readfirstlane(c);
+}
+
+template <int WS, int TEAM, int G, int MODE, int LB, int TL = 0, int PS = 0>
 __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(EncodeArgs a) {
     using Lay = EncLayout<WS, TEAM>;
     constexpr int W = Lay::W;
     __shared__ __attribute__((aligned(16))) uint8_t smem[Lay::BYTES];
-    if constexpr (TL == 4) {
-        const uint32_t lj = blockIdx.x;  // one large message per workgroup
-        const uint32_t msg = a.lmeta[lj].msg;
-        if (msg != kNone) encode_one<WS, TEAM, G, MODE, LB, TL>(a, smem, msg, lj, 0);
-    } else if constexpr (TL > 0) {
-        const uint32_t i = a.list_base + blockIdx.x;  // one span (TL 1) or tile per workgroup
-        const uint64_t e = TL == 1 ? a.spans[i] : a.tiles[i];
-        const uint32_t lj = (uint32_t)e;
-        if (lj == kNone) return;  // a message that did not fit the budgets
-        encode_one<WS, TEAM, G, MODE, LB, TL>(a, smem, a.lmeta[lj].msg, lj, (uint32_t)(e >> 32));
-    } else if constexpr (LB) {
+    if constexpr (LB) {
         uint32_t *misc = reinterpret_cast<uint32_t *>(smem + Lay::OFF_MISC);
         if (threadIdx.x == 0) misc[M_MSG] = atomicAdd(a.ticket, 1u);
         team_sync<W>();
         encode_one<WS, TEAM, G, MODE, LB, 0>(a, smem, __builtin_amdgcn_readfirstlane(misc[M_MSG]), 0, 0);
+        return;
     } else {
-        if (!a.list) {
-            encode_one<WS, TEAM, G, MODE, LB, 0>(a, smem, blockIdx.x, 0, 0);
-            return;
+        // (slotted launches always pass a class list)
+        auto one = [&](uint32_t i) __attribute__((always_inline)) {
+            if constexpr (TL == 0) {
+                encode_one<WS, TEAM, G, MODE, LB, 0>(a, smem, a.list[i], 0, 0);
+            } else if constexpr (TL == 4) {
+                const uint32_t msg = a.lmeta[i].msg;  // one large message per workgroup
+                if (msg != kNone) encode_one<WS, TEAM, G, MODE, LB, TL>(a, smem, msg, i, 0);
+            } else {
+                const uint64_t e = TL == 1 ? a.spans[i] : a.tiles[i];  // one span (TL 1) or tile
+                const uint32_t lj = (uint32_t)e;
+                if (lj == kNone) return;  // a message that did not fit the budgets
+                encode_one<WS, TEAM, G, MODE, LB, TL>(a, smem, a.lmeta[lj].msg, lj, (uint32_t)(e >> 32));
+            }
+        };
+        const uint32_t cnt = entry_count<TL>(a);
+        const uint32_t i0 = a.list_base + blockIdx.x;
+        if constexpr (PS) {
+            for (uint32_t i = i0; i < cnt; i += gridDim.x) {
+                if (i != i0) team_sync<W>();  // the previous entry is done with the LDS
+                one(i);
+            }
+        } else {
+            if (i0 >= cnt) return;
+            one(i0);
         }
-        // one class-list entry per workgroup (grids sized from the plan's counts; workgroups
-        // past the count, if any, exit at once)
-        const uint32_t i = a.list_base + blockIdx.x;
-        if (i < *a.list_count) encode_one<WS, TEAM, G, MODE, LB, 0>(a, smem, a.list[i], 0, 0);
     }
 }
 
@@ -1554,12 +1577,15 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
 struct PlanArgs {
     const uint64_t *in_off;
     uint32_t n_msgs;
-    unsigned long long *cnt;  // [0] small, [1] medium, [2] large entries, [3] tiles, [4] spans claimed
+    // [0] small (listed), [1] medium, [2] large entries, [3] tiles, [4] spans claimed, [5] small
+    // messages (listed or not: the host's count history switches the small class back on)
+    unsigned long long *cnt;
     uint32_t *slist, *mlist;
     uint64_t *tiles, *spans;
     LMeta *lmeta;
-    uint32_t lmax, tile_cap;  // span_cap = tile_cap / kSpanTiles
+    uint32_t lmax, tile_cap;  // span_cap = tile_cap / kSpanTiles (0, 0: no tiled path)
     uint64_t small_max, large_min;
+    uint32_t small_on;  // 0: small messages join the medium list
 };
 
 constexpr uint32_t kPlanThreads = 1024, kPlanPer = 2;  // messages per plan workgroup: 2048
@@ -1580,7 +1606,7 @@ __global__ __launch_bounds__(kPlanThreads) void tdt_encode_plan_kernel(PlanArgs 
     wg_claim<kPlanPer>(isl, j, p.cnt + 2, lds);
     wg_claim<kPlanPer>(T, t0, p.cnt + 3, lds);
     wg_claim<kPlanPer>(S, s0, p.cnt + 4, lds);
-    uint64_t sm[kPlanPer], md[kPlanPer], ps[kPlanPer], pm[kPlanPer];
+    uint64_t sm[kPlanPer], md[kPlanPer], ps[kPlanPer], pm[kPlanPer], sc[kPlanPer], pc[kPlanPer];
 #pragma unroll
     for (int k = 0; k < (int)kPlanPer; ++k) {
         const uint32_t i = (blockIdx.x * kPlanPer + k) * kPlanThreads + threadIdx.x;
@@ -1604,11 +1630,14 @@ __global__ __launch_bounds__(kPlanThreads) void tdt_encode_plan_kernel(PlanArgs 
                 p.spans[s0[k] + t] = large ? (t << 32 | j[k]) : (uint64_t)kNone;
         }
         const bool valid = i < p.n_msgs;
-        sm[k] = valid && !large && n[k] <= p.small_max ? 1u : 0u;
-        md[k] = valid && !large && n[k] > p.small_max ? 1u : 0u;
+        const bool small = valid && !isl[k] && n[k] <= p.small_max;
+        sc[k] = small ? 1u : 0u;
+        sm[k] = small && p.small_on ? 1u : 0u;
+        md[k] = valid && !large && !sm[k] ? 1u : 0u;
     }
     wg_claim<kPlanPer>(sm, ps, p.cnt + 0, lds);
     wg_claim<kPlanPer>(md, pm, p.cnt + 1, lds);
+    wg_claim<kPlanPer>(sc, pc, p.cnt + 5, lds);
 #pragma unroll
     for (int k = 0; k < (int)kPlanPer; ++k) {
         const uint32_t i = (blockIdx.x * kPlanPer + k) * kPlanThreads + threadIdx.x;
@@ -1709,10 +1738,12 @@ __global__ __launch_bounds__(64) void tdt_encode_lscan_kernel(EncodeArgs a, cons
 // The kernel instances of one word size.  The product library instantiates them in
 // tdt_enc_ws.hip, one translation unit per word size (compiled in parallel), and tdt_api.hip
 // declares them extern; diagnostic single-TU builds instantiate them implicitly.
-#define PSY_ENC_INSTANCES(X, WS)                                                                      \
-    X(WS, 512, 8, MODE_ENCODE, 0, 0) X(WS, 512, 8, MODE_ENCODE, 0, 1) X(WS, 512, 8, MODE_ENCODE, 0, 2) \
-    X(WS, 512, 8, MODE_ENCODE, 0, 3) X(WS, 512, 8, MODE_ENCODE, 0, 4) X(WS, 64, 4, MODE_ENCODE, 0, 0)  \
-    X(WS, 64, 4, MODE_ENCODE, 1, 0) X(WS, 512, 8, MODE_ENCODE, 1, 0) X(WS, 64, 4, MODE_MAPPED, 1, 0)   \
-    X(WS, 512, 8, MODE_MAPPED, 1, 0) X(WS, 64, 4, MODE_ANALYZE, 1, 0) X(WS, 512, 8, MODE_ANALYZE, 1, 0)
+#define PSY_ENC_INSTANCES(X, WS)                                                                         \
+    X(WS, 512, 8, MODE_ENCODE, 0, 0, 0) X(WS, 512, 8, MODE_ENCODE, 0, 1, 0) X(WS, 512, 8, MODE_ENCODE, 0, 2, 0) \
+    X(WS, 512, 8, MODE_ENCODE, 0, 3, 0) X(WS, 512, 8, MODE_ENCODE, 0, 4, 0) X(WS, 64, 4, MODE_ENCODE, 0, 0, 0)  \
+    X(WS, 512, 8, MODE_ENCODE, 0, 0, 1) X(WS, 512, 8, MODE_ENCODE, 0, 1, 1) X(WS, 512, 8, MODE_ENCODE, 0, 2, 1) \
+    X(WS, 512, 8, MODE_ENCODE, 0, 3, 1) X(WS, 512, 8, MODE_ENCODE, 0, 4, 1) X(WS, 64, 4, MODE_ENCODE, 0, 0, 1)  \
+    X(WS, 64, 4, MODE_ENCODE, 1, 0, 0) X(WS, 512, 8, MODE_ENCODE, 1, 0, 0) X(WS, 64, 4, MODE_MAPPED, 1, 0, 0)   \
+    X(WS, 512, 8, MODE_MAPPED, 1, 0, 0) X(WS, 64, 4, MODE_ANALYZE, 1, 0, 0) X(WS, 512, 8, MODE_ANALYZE, 1, 0, 0)
 
 }  // namespace psy

@@ -248,11 +248,16 @@ class TdtCodec:
                                           _ptr(st), self._stream(stream)))
         return hist[:n], ent[:n], mp[:n], st[:n]
 
-    def error_flags(self) -> int:
-        """Device invariant flags (tdt_ctx_error_flags; 0 for a correct build).  Synchronises."""
+    def error_flags(self, stream=None) -> int:
+        """Device invariant flags (tdt_ctx_error_flags; 0 for a correct build).  Synchronises
+        the stream the batches were issued on (default: the current torch stream)."""
         fl = C.c_uint32(0)
-        check(self._lib.tdt_ctx_error_flags(self._h, C.byref(fl)))
+        check(self._lib.tdt_ctx_error_flags(self._h, self._stream(stream), C.byref(fl)))
         return int(fl.value)
+
+    def set_option(self, option: int, value: int):
+        """tdt_ctx_set_option (tuning / diagnostic knobs; results are the same bytes)."""
+        check(self._lib.tdt_ctx_set_option(self._h, option, int(value)))
 
     # ---- host path (socket buffers) -------------------------------------------------------
     def encode_host(self, data: np.ndarray, offsets: np.ndarray):

@@ -3,10 +3,9 @@
 Batches holding a message (or decoded blob) longer than 64 KiB take the two-phase path
 (slotted message-class kernels, scan of the lengths, gather into the compacted buffer — or, for
 decode, sizes + scan then the slotted kernels writing in place); the rest take the look-back
-kernel.  Both must give the same bytes, offsets and statuses (PSYNE_TDT_NO_TWO_PHASE=1 forces
+kernel.  Both must give the same bytes, offsets and statuses (TDT_OPT_NO_TWO_PHASE forces
 the look-back path), every blob must equal the oracle's, and the capacity semantics of the
 compacted API (`out_cap` smaller than the total) must match too."""
-import os
 
 import numpy as np
 import pytest
@@ -45,15 +44,16 @@ def _batch(seed):
     return msgs, np.concatenate(msgs), off
 
 
-def _both(fn):
+def _both(codec, fn):
     """fn() under the two-phase path and under the forced look-back path."""
-    os.environ.pop("PSYNE_TDT_NO_TWO_PHASE", None)
+    from psyne_amd._lib import TDT_OPT_NO_TWO_PHASE
+    codec.set_option(TDT_OPT_NO_TWO_PHASE, 0)
     a = fn()
-    os.environ["PSYNE_TDT_NO_TWO_PHASE"] = "1"
+    codec.set_option(TDT_OPT_NO_TWO_PHASE, 1)
     try:
         b = fn()
     finally:
-        os.environ.pop("PSYNE_TDT_NO_TWO_PHASE", None)
+        codec.set_option(TDT_OPT_NO_TWO_PHASE, 0)
     return a, b
 
 
@@ -69,7 +69,7 @@ def test_two_phase_matches_lookback_and_oracle(seed):
         torch.cuda.synchronize()
         return out.cpu().numpy(), eoff.cpu().numpy(), st.cpu().numpy()
 
-    (b1, o1, s1), (b2, o2, s2) = _both(enc)
+    (b1, o1, s1), (b2, o2, s2) = _both(codec, enc)
     assert (s1 == 0).all() and (s2 == 0).all()
     assert np.array_equal(o1, o2)
     assert np.array_equal(b1[:o1[-1]], b2[:o2[-1]])
@@ -87,7 +87,7 @@ def test_two_phase_matches_lookback_and_oracle(seed):
         torch.cuda.synchronize()
         return out.cpu().numpy(), doff.cpu().numpy(), st.cpu().numpy()
 
-    (d1, p1, t1), (d2, p2, t2) = _both(dec)
+    (d1, p1, t1), (d2, p2, t2) = _both(codec, dec)
     assert (t1 == 0).all() and (t2 == 0).all()
     assert np.array_equal(p1, off) and np.array_equal(p2, off)
     assert np.array_equal(d1[:off[-1]], data) and np.array_equal(d2[:off[-1]], data)
@@ -111,7 +111,7 @@ def test_two_phase_capacity_semantics():
         torch.cuda.synchronize()
         return out.cpu().numpy(), eoff.cpu().numpy(), st.cpu().numpy()
 
-    (b1, o1, s1), (b2, o2, s2) = _both(enc)
+    (b1, o1, s1), (b2, o2, s2) = _both(codec, enc)
     assert np.array_equal(o1, o2) and np.array_equal(s1, s2)
     assert (s1 == 5).any() and (s1 == 0).any()
     for i in range(len(msgs)):
@@ -134,11 +134,12 @@ def test_compacted_under_graph_capture():
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(s):                        # warm the look-back path's scratch
-        os.environ["PSYNE_TDT_NO_TWO_PHASE"] = "1"
+        from psyne_amd._lib import TDT_OPT_NO_TWO_PHASE
+        codec.set_option(TDT_OPT_NO_TWO_PHASE, 1)
         try:
             codec.encode_batch(d, o, out=out, out_offsets=eoff, status=st)
         finally:
-            os.environ.pop("PSYNE_TDT_NO_TWO_PHASE", None)
+            codec.set_option(TDT_OPT_NO_TWO_PHASE, 0)
     torch.cuda.current_stream().wait_stream(s)
     torch.cuda.synchronize()
     out.zero_()

@@ -3,7 +3,6 @@ mapping pass, per-tile counts, the scan that stitches the run carried across til
 (255-cap chunk starts inside the next tile), and the emit pass — every blob compared with the
 oracle byte for byte, then decoded back.  Also the fallback to the whole-message kernel when
 the tile budget is spent."""
-import os
 
 import numpy as np
 import pytest
@@ -129,11 +128,9 @@ def test_large_uncompressible_passthrough():
 def test_tile_budget_fallback():
     """A tile budget of 64 tiles (4 MiB): the first large messages take the tiled path, the
     rest the whole-message kernel — the blobs are the same either way."""
-    os.environ["PSYNE_TDT_TILE_CAP"] = "64"
-    try:
-        codec = codec_for(4)
-    finally:
-        del os.environ["PSYNE_TDT_TILE_CAP"]
+    from psyne_amd._lib import TDT_OPT_TILE_CAP
+    codec = codec_for(4)
+    codec.set_option(TDT_OPT_TILE_CAP, 64)
     rng = np.random.default_rng(17)
     msgs = [runs_message(rng, int(rng.integers(5, 20)) * 65536 + 4 * k, 280) for k in range(12)]
     check_batch(msgs, codec=codec)

@@ -322,19 +322,17 @@ def test_roundtrip_many_64k():
 
 
 @pytest.mark.parametrize("path", ["lookback", "two_phase"])
-def test_many_tiny_lookback(path, monkeypatch):
+def test_many_tiny_lookback(path):
     # 200k UNCP messages: the look-back chain at depth (forced: small-message batches take the
     # two-phase compaction by default) and the two-phase path's scan + gather
-    if path == "lookback":
-        monkeypatch.setenv("PSYNE_TDT_NO_TWO_PHASE", "1")
-    else:
-        monkeypatch.delenv("PSYNE_TDT_NO_TWO_PHASE", raising=False)
+    from psyne_amd._lib import TDT_OPT_NO_TWO_PHASE
     rng = np.random.default_rng(22)
     sizes = rng.integers(0, 40, 200000)
     data = rng.integers(0, 256, int(sizes.sum()), dtype=np.uint8)
     off = np.zeros(sizes.size + 1, np.int64)
     off[1:] = np.cumsum(sizes)
     codec = make_codec(hint=64)
+    codec.set_option(TDT_OPT_NO_TWO_PHASE, 1 if path == "lookback" else 0)
     enc, eoff, st = codec.encode_batch(torch.from_numpy(data).cuda(), torch.from_numpy(off).cuda())
     torch.cuda.synchronize()
     eo = eoff.cpu().numpy()
