@@ -61,7 +61,10 @@ def parse():
                     help="target duration of EACH of the four CPU-baseline rows (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = all usable host cores")
     ap.add_argument("--cpu-kind", choices=["reference", "port"], default="reference")
-    ap.add_argument("--host-inclusive", action="store_true", help="also time pinned H2D+kernel+D2H")
+    ap.add_argument("--host-inclusive", action="store_true",
+                    help="also time host buffers (pinned and pageable) through H2D+kernel+D2H")
+    ap.add_argument("--latency", action="store_true",
+                    help="also time one message per call (1 KiB / 64 KiB / 1 MiB) against the reference CPU codec")
     ap.add_argument("--compacted-steps", type=int, default=3,
                     help="timed steps of the compacted (look-back) API leg after the headline (0 = skip)")
     ap.add_argument("--seed", type=int, default=None)
@@ -185,16 +188,33 @@ def host_cores():
     return nproc, phys
 
 
+def affinity_desc():
+    """(cpu count, compact list) of this process's CPU affinity mask."""
+    cpus = sorted(os.sched_getaffinity(0))
+    runs, start = [], None
+    for i, c in enumerate(cpus):
+        if start is None:
+            start = c
+        if i + 1 == len(cpus) or cpus[i + 1] != c + 1:
+            runs.append("%d-%d" % (start, c) if c > start else "%d" % c)
+            start = None
+    return len(cpus), ",".join(runs)
+
+
 def cpu_baseline(data_u8, msg_bytes, target_s, threads, kind):
-    """Four CPU rows of the REFERENCE codec (oracle/_ref, the reference header compiled where it
-    lies) on a bounded sample of the same messages: {1, `threads`} threads x sample_fraction
-    {0.3 (reference default), 1.0 (parity mode)}; one protocol object per thread."""
+    """CPU rows of the REFERENCE codec (oracle/_ref, the reference header compiled where it lies)
+    on bounded samples of the same messages: {1, `threads`} threads x sample_fraction {0.3
+    (reference default), 1.0 (parity mode)}; one protocol object per thread.  The multi-thread
+    rows run over 4 GiB of DISTINCT messages (one pass: no cache-resident working set); the
+    1-thread rows over as many distinct messages as take about `target_s`."""
     import numpy as np
     from oracle.oracle import Oracle, Reference
-    n_sample = 512
-    sample = data_u8[: n_sample * msg_bytes].cpu().numpy()
-    off = np.arange(n_sample + 1, dtype=np.uint64) * msg_bytes
+    n_all = data_u8.numel() // msg_bytes
+    n_big = min(n_all, max(1, (4 << 30) // msg_bytes))
+    sample = data_u8[: n_big * msg_bytes].cpu().numpy()
+    off = np.arange(n_big + 1, dtype=np.uint64) * msg_bytes
     nproc, phys = host_cores()
+    aff_n, aff = affinity_desc()
     rows = []
     if kind == "reference":
         if not Reference.available():
@@ -206,30 +226,33 @@ def cpu_baseline(data_u8, msg_bytes, target_s, threads, kind):
             t1, _ = ref.bench(sample[: 16 * msg_bytes], off[:17], sample_fraction=sf, threads=1, reps=1)
             per_msg = t1 / 16
             for thr in (1, threads):
-                reps = max(1, int(target_s * thr / (per_msg * n_sample)))
-                secs, enc = ref.bench(sample, off, sample_fraction=sf, threads=thr, reps=reps)
-                payload = n_sample * msg_bytes * reps
+                k = n_big if thr > 1 else int(min(n_big, max(16, target_s / per_msg)))
+                secs, enc = ref.bench(sample[: k * msg_bytes], off[: k + 1], sample_fraction=sf, threads=thr, reps=1)
+                payload = k * msg_bytes
                 rows.append(dict(value=payload / secs / 2**30, unit="GiB/s", cores=thr, sample_fraction=sf,
-                                 seconds=round(secs, 2), msgs=n_sample * reps, ratio=float(payload / enc)))
+                                 seconds=round(secs, 2), msgs=k, distinct_bytes=payload, ratio=float(payload / enc)))
         main = next(r for r in rows if r["sample_fraction"] == 0.3 and r["cores"] == threads)
         return dict(value=main["value"], unit="GiB/s", cores=threads, kind="reference",
-                    sample="%d x %d B messages (the benched payload's first %d), reference "
-                           "TDTCompressionProtocol encode+decode, default TDTConfig (sample_fraction 0.3), "
-                           "one object per thread, %d threads, %.1f s" % (n_sample, msg_bytes, n_sample, threads,
-                                                                         main["seconds"]),
-                    rows=rows, nproc=nproc, lscpu_physical_cores=phys)
+                    sample="%d distinct x %d B messages (the benched payload's first %.1f GiB, one pass), reference "
+                           "TDTCompressionProtocol encode+decode, default TDTConfig (sample_fraction 0.3), one "
+                           "object per thread, %d threads, %.1f s" % (main["msgs"], msg_bytes,
+                                                                      main["distinct_bytes"] / 2**30, threads,
+                                                                      main["seconds"]),
+                    rows=rows, nproc=nproc, lscpu_physical_cores=phys, affinity_cpus=aff_n, affinity_mask=aff,
+                    threads_note="threads = this process's affinity (%d CPUs: %s) capped by OMP_NUM_THREADS; "
+                                 "the host has %s physical cores" % (aff_n, aff, phys))
     orc = Oracle()
     t0 = time.perf_counter()
-    reps = 0
-    while time.perf_counter() - t0 < target_s:
-        for i in range(n_sample):
-            b = orc.encode(sample[off[i]:off[i + 1]], bandwidth=10.0)
-            orc.decode(b)
-        reps += 1
+    k = 0
+    while time.perf_counter() - t0 < target_s and k < n_big:
+        b = orc.encode(sample[off[k]:off[k + 1]], bandwidth=10.0)
+        orc.decode(b)
+        k += 1
     secs = time.perf_counter() - t0
-    return dict(value=n_sample * msg_bytes * reps / secs / 2**30, unit="GiB/s", cores=1, kind="port",
-                sample="%d x %d B messages x %d reps, oracle C restatement (sample_fraction 1.0), 1 thread"
-                       % (n_sample, msg_bytes, reps), nproc=nproc, lscpu_physical_cores=phys)
+    return dict(value=k * msg_bytes / secs / 2**30, unit="GiB/s", cores=1, kind="port",
+                sample="%d distinct x %d B messages, oracle C restatement (sample_fraction 1.0), 1 thread"
+                       % (k, msg_bytes), nproc=nproc, lscpu_physical_cores=phys, affinity_cpus=aff_n,
+                affinity_mask=aff)
 
 
 def pcie_ceiling(torch, dev, nbytes=256 << 20, reps=5):
@@ -267,40 +290,103 @@ def pcie_ceiling(torch, dev, nbytes=256 << 20, reps=5):
 
 
 def host_inclusive(torch, codec, data, off, n, mb, reps=3):
-    """The TCP socket-buffer path: pinned host payloads -> tdt_encode_host (chunked, two
-    streams: H2D, kernel and D2H of neighbouring chunks overlap) -> pinned host blobs ->
-    tdt_decode_host -> pinned host payloads.  GiB/s of payload per direction, best of reps."""
+    """The TCP socket-buffer path: host payloads -> tdt_encode_host (64 MiB chunks on two
+    streams: H2D, kernel and D2H of neighbouring chunks overlap) -> host blobs -> tdt_decode_host
+    -> host payloads.  Two callers: PINNED buffers (DMA'd directly) and PAGEABLE ones (numpy
+    arrays, as a socket buffer or std::vector is: staged through the context's pinned buffers by
+    its copy threads).  GiB/s of payload per direction, best of reps."""
+    import numpy as np
     from psyne_amd._lib import check
     lib, h = codec._lib, codec._h
     m = min(n, 32768)
-    src = torch.empty(m * mb, dtype=torch.uint8, pin_memory=True)
-    src.copy_(data[: m * mb])
-    hoff = torch.arange(m + 1, dtype=torch.int64) * mb
-    cap = m * codec.encode_bound(mb)
-    henc = torch.empty(cap, dtype=torch.uint8, pin_memory=True)
-    heoff = torch.empty(m + 1, dtype=torch.int64)
-    hst = torch.empty(m, dtype=torch.int32)
-    hdec = torch.empty(m * mb, dtype=torch.uint8, pin_memory=True)
-    hdoff = torch.empty(m + 1, dtype=torch.int64)
-    hdst = torch.empty(m, dtype=torch.int32)
-    torch.cuda.synchronize()
-    te, td = [], []
-    for _ in range(reps):
-        t0 = time.perf_counter()
-        check(lib.tdt_encode_host(h, src.data_ptr(), hoff.data_ptr(), m, henc.data_ptr(), cap, heoff.data_ptr(),
-                                  hst.data_ptr()))
-        te.append(time.perf_counter() - t0)
-        nb = int(heoff[-1])
-        t0 = time.perf_counter()
-        check(lib.tdt_decode_host(h, henc.data_ptr(), heoff.data_ptr(), m, hdec.data_ptr(), m * mb, hdoff.data_ptr(),
-                                  hdst.data_ptr()))
-        td.append(time.perf_counter() - t0)
-    ok = bool(torch.equal(hdec, src)) and int(hst.abs().sum()) == 0 and int(hdst.abs().sum()) == 0
     b = m * mb
-    return {"msgs": m, "encode_GiBps": round(b / min(te) / 2**30, 3), "decode_GiBps": round(b / min(td) / 2**30, 3),
-            "roundtrip_GiBps": round(b / (min(te) + min(td)) / 2**30, 3), "encoded_bytes": nb, "ok": ok,
-            "note": "pinned host buffers; C-ABI tdt_encode_host/tdt_decode_host: 256 MiB chunks on two streams "
-                    "(H2D, kernel, D2H overlapped); payload bytes / wall"}
+    hoff = np.arange(m + 1, dtype=np.uint64) * mb
+    cap = m * codec.encode_bound(mb)
+    heoff = np.zeros(m + 1, np.uint64)
+    hst = np.zeros(m, np.int32)
+    hdoff = np.zeros(m + 1, np.uint64)
+    hdst = np.zeros(m, np.int32)
+    out = {"msgs": m}
+    for kind in ("pinned", "pageable"):
+        if kind == "pinned":
+            t_src = torch.empty(b, dtype=torch.uint8, pin_memory=True)
+            t_src.copy_(data[:b])
+            t_enc = torch.empty(cap, dtype=torch.uint8, pin_memory=True)
+            t_dec = torch.empty(b, dtype=torch.uint8, pin_memory=True)
+            src, enc, dec = t_src.numpy(), t_enc.numpy(), t_dec.numpy()
+        else:
+            src = data[:b].cpu().numpy().copy()
+            enc = np.empty(cap, np.uint8)
+            dec = np.empty(b, np.uint8)
+        enc[:] = 0  # touch the pages (a socket buffer's pages are resident)
+        dec[:] = 0
+        torch.cuda.synchronize()
+        te, td = [], []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            check(lib.tdt_encode_host(h, src.ctypes.data, hoff.ctypes.data, m, enc.ctypes.data, cap,
+                                      heoff.ctypes.data, hst.ctypes.data))
+            te.append(time.perf_counter() - t0)
+            nb = int(heoff[-1])
+            t0 = time.perf_counter()
+            check(lib.tdt_decode_host(h, enc.ctypes.data, heoff.ctypes.data, m, dec.ctypes.data, b, hdoff.ctypes.data,
+                                      hdst.ctypes.data))
+            td.append(time.perf_counter() - t0)
+        ok = bool(np.array_equal(dec, src)) and int(np.abs(hst).sum()) == 0 and int(np.abs(hdst).sum()) == 0
+        out[kind] = {"encode_GiBps": round(b / min(te) / 2**30, 3), "decode_GiBps": round(b / min(td) / 2**30, 3),
+                     "roundtrip_GiBps": round(b / (min(te) + min(td)) / 2**30, 3), "encoded_bytes": nb, "ok": ok}
+    out["pageable_vs_pinned"] = round(out["pageable"]["roundtrip_GiBps"] / out["pinned"]["roundtrip_GiBps"], 3)
+    out["note"] = ("C-ABI tdt_encode_host/tdt_decode_host, %d x %d B; payload bytes / wall; pageable buffers staged "
+                   "by %s copy threads" % (m, mb, os.environ.get("PSYNE_TDT_COPY_THREADS", "the default")))
+    return out
+
+
+def message_latency(torch, codec, data, sizes=(1024, 65536, 1 << 20), calls=200):
+    """One message per call, as the reference's Protocol::encode / decode are called
+    (protocol_demo.cpp:135-189): tdt_encode_host + tdt_decode_host on a pageable buffer (the
+    HipTDTCompressionProtocol path), median microseconds per call; beside it the reference codec
+    on one host thread (oracle/_ref), microseconds per message, default and parity config."""
+    import numpy as np
+    from oracle.oracle import Reference
+    from psyne_amd._lib import check
+    lib, h = codec._lib, codec._h
+    ref = Reference() if Reference.available() else None
+    rows = []
+    for n in sizes:
+        src = data[:n].cpu().numpy().copy()
+        off = np.array([0, n], np.uint64)
+        cap = codec.encode_bound(n)
+        enc = np.empty(cap, np.uint8)
+        eoff = np.zeros(2, np.uint64)
+        dec = np.empty(n, np.uint8)
+        doff = np.zeros(2, np.uint64)
+        st = np.zeros(1, np.int32)
+        te, td = [], []
+        for i in range(calls + 5):
+            t0 = time.perf_counter()
+            check(lib.tdt_encode_host(h, src.ctypes.data, off.ctypes.data, 1, enc.ctypes.data, cap, eoff.ctypes.data,
+                                      st.ctypes.data))
+            t1 = time.perf_counter()
+            check(lib.tdt_decode_host(h, enc.ctypes.data, eoff.ctypes.data, 1, dec.ctypes.data, n, doff.ctypes.data,
+                                      st.ctypes.data))
+            t2 = time.perf_counter()
+            if i >= 5:
+                te.append(t1 - t0)
+                td.append(t2 - t1)
+        row = {"bytes": n, "gpu_encode_us": round(float(np.median(te)) * 1e6, 1),
+               "gpu_decode_us": round(float(np.median(td)) * 1e6, 1), "ok": bool(np.array_equal(dec, src))}
+        if ref is not None:
+            k = max(4, min(256, (64 << 20) // n))
+            rep = np.tile(src, k)
+            roff = np.arange(k + 1, dtype=np.uint64) * n
+            for sf in (0.3, 1.0):
+                secs, _ = ref.bench(rep, roff, sample_fraction=sf, threads=1, reps=1)
+                row["ref_cpu_us_sf%.1f" % sf] = round(secs / k * 1e6, 1)
+        row["gpu_roundtrip_us"] = round(row["gpu_encode_us"] + row["gpu_decode_us"], 1)
+        rows.append(row)
+    return {"rows": rows, "note": "one message per call: GPU = tdt_encode_host + tdt_decode_host (pageable buffers; "
+                                  "H2D, kernel, D2H per call), median of %d; reference = the compiled reference "
+                                  "codec, encode+decode per message on one host thread (ref_cpu_us_*)" % calls}
 
 
 def gather_obj(obj, world):
@@ -476,6 +562,7 @@ def main():
     if a.host_inclusive and a.workload != "c4":
         host = host_inclusive(torch, codec, data, off, n, mb)
         host["pcie_ceiling"] = pcie_ceiling(torch, dev)
+    latency = message_latency(torch, codec, data) if a.latency and rank == 0 else None
     per_rank = gather_obj({"rank": rank, "device": my_dev, "msgs": n, "payload_bytes": payload,
                            "GiBps": round(my_rate, 3), "kernels_ms": [round(t_enc, 4), round(t_dec, 4)],
                            "host_inclusive": host}, world)
@@ -549,6 +636,8 @@ def main():
             line["compacted"] = compacted
         if host:
             line["host_inclusive"] = host
+        if latency:
+            line["message_latency"] = latency
         if shared:
             line["rehearsal"] = "all ranks on device 0 over gloo (PSYNE_BENCH_SHARED_DEVICE=1): not a scaling number"
         print(json.dumps(line), flush=True)

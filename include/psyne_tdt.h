@@ -182,14 +182,14 @@ int tdt_ctx_error_flags(tdt_ctx *ctx, void *hip_stream, uint32_t *flags);
 
 /* Tuning / diagnostic options (tdt_ctx_create reads the same from the environment once:
  * PSYNE_TDT_LARGE_MIN, PSYNE_TDT_TILE_CAP, PSYNE_TDT_NO_SIDE, PSYNE_TDT_SMALL_MAIN,
- * PSYNE_TDT_NO_TWO_PHASE).  Not needed for correct results: every setting encodes and decodes
+ * PSYNE_TDT_NO_TWO_PHASE, PSYNE_TDT_COPY_THREADS).  Not needed for correct results: every setting encodes and decodes
  * the same bytes. */
 #define TDT_OPT_LARGE_MIN 1               /* messages above this many bytes take the tiled path */
 #define TDT_OPT_TILE_CAP 2                /* lower tile budget per batch (tests of the fallback) */
 #define TDT_OPT_NO_SIDE_STREAM 3          /* 1: the tile pipeline runs on the caller's stream */
 #define TDT_OPT_SMALL_ON_CALLER_STREAM 4  /* 1: small-message lists stay on the caller's stream */
 #define TDT_OPT_NO_TWO_PHASE 5            /* 1: compacted calls always take the one-pass kernels */
-#define TDT_OPT_COPY_THREADS 6            /* host threads staging pageable buffers (default <= 8) */
+#define TDT_OPT_COPY_THREADS 6            /* host threads staging pageable buffers (default <= 16) */
 int tdt_ctx_set_option(tdt_ctx *ctx, int option, uint64_t value);
 
 /* Host-memory analyze (analyze_data :206-222): h_entropy n*ws doubles, h_mapping n*ws int32

@@ -1151,10 +1151,12 @@ int tdt_ctx_create(int device, const tdt_config *cfg, tdt_ctx **out) {
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
         x->cus = cus;
-    // staging-copy threads: up to 8, within this process's CPU affinity
+    // staging-copy threads: up to 16, within this process's CPU affinity (PSYNE_TDT_COPY_THREADS)
     cpu_set_t cs;
     CPU_ZERO(&cs);
-    if (sched_getaffinity(0, sizeof(cs), &cs) == 0) x->copy_threads = std::max(1, std::min(8, CPU_COUNT(&cs)));
+    if (sched_getaffinity(0, sizeof(cs), &cs) == 0) x->copy_threads = std::max(1, std::min(16, CPU_COUNT(&cs)));
+    if (const char *e = std::getenv("PSYNE_TDT_COPY_THREADS"))
+        x->copy_threads = std::max(1, std::min(64, (int)std::strtol(e, nullptr, 10)));
     *out = x;
     return TDT_OK;
 }

@@ -167,6 +167,35 @@ __device__ __forceinline__ double row_sum_f64(double x) {
     x += dpp_f64<0x118>(x);  // row_shr:8
     return x;
 }
+// Segmented sums over SEG consecutive lanes (SEG a power of two, 1..64): the segment's last
+// lane receives its sum (other lanes: partial sums).  row_shr steps stay inside 16-lane rows;
+// row_bcast:15 / :31 carry row sums across rows.
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ double dpp_f64_rm(double x) {
+    const uint64_t u = __builtin_bit_cast(uint64_t, x);
+    const uint32_t lo = dpp_mov<CTRL, ROWMASK>((uint32_t)u), hi = dpp_mov<CTRL, ROWMASK>((uint32_t)(u >> 32));
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+template <int SEG>
+__device__ __forceinline__ double seg_sum_f64(double x) {
+    if constexpr (SEG >= 2) x += dpp_f64_rm<0x111, 0xf>(x);  // row_shr:1
+    if constexpr (SEG >= 4) x += dpp_f64_rm<0x112, 0xf>(x);  // row_shr:2
+    if constexpr (SEG >= 8) x += dpp_f64_rm<0x114, 0xf>(x);  // row_shr:4
+    if constexpr (SEG >= 16) x += dpp_f64_rm<0x118, 0xf>(x);  // row_shr:8
+    if constexpr (SEG >= 32) x += dpp_f64_rm<0x142, 0xa>(x);  // row_bcast:15 into rows 1, 3
+    if constexpr (SEG >= 64) x += dpp_f64_rm<0x143, 0xc>(x);  // row_bcast:31 into rows 2, 3
+    return x;
+}
+template <int SEG>
+__device__ __forceinline__ uint32_t seg_sum_u32(uint32_t x) {
+    if constexpr (SEG >= 2) x += dpp_mov<0x111, 0xf>(x);
+    if constexpr (SEG >= 4) x += dpp_mov<0x112, 0xf>(x);
+    if constexpr (SEG >= 8) x += dpp_mov<0x114, 0xf>(x);
+    if constexpr (SEG >= 16) x += dpp_mov<0x118, 0xf>(x);
+    if constexpr (SEG >= 32) x += dpp_mov<0x142, 0xa>(x);
+    if constexpr (SEG >= 64) x += dpp_mov<0x143, 0xc>(x);
+    return x;
+}
 __device__ __forceinline__ double readlane_f64(double x, int l) {
     const uint64_t u = __builtin_bit_cast(uint64_t, x);
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, l);

@@ -173,10 +173,89 @@ struct EncLayout {
 enum {
     M_MSG = 0, M_NS = 1, M_L0 = 2, M_K0 = 3, M_K1 = 4, M_SELA = 8 /*4*/, M_SELB = 12 /*4*/, M_EDA = 16,
     M_EDB = 17, M_EXACT = 18, M_STATUS = 26, M_MAP = 32 /*16*/, M_ENT = 64 /*16 doubles*/, M_BASE = 96 /*u64*/,
-    M_SB = 100 /*16*/, M_PART = 128 /*16 doubles: per-wave entropy partials*/
+    M_SB = 100 /*16*/, M_PART = 128 /*16 doubles: per-wave entropy partials*/, M_Z = 48 /*16: zero-bin totals*/,
+    M_MAPBITS = 5 /*bit b = mapping[b]*/
 };
-// decision margin of the mapping fast path (>= 2000x the worst-case |fma chain - any-order sum|)
-constexpr double kTieMargin = 1e-9;
+// decision margin of the mapping fast path, in bits of entropy (> 2x its worst-case error)
+constexpr double kFastMargin = 1e-4;
+
+// The slot layout of a byte-plane mapping (separate_byte_streams :527-549): slot j < L0 of a
+// 16-byte group is stream-0 byte j (word j / k0, position = the (j % k0)-th position mapped to
+// 0), slot j >= L0 stream-1 byte j - L0; selA / selB are the v_perm selectors that gather T
+// (slot 4t + q in byte t of T[q]) from the group's dwords (x,y) / (z,w); edA / edB the edges
+// word (byte 0: stream 0's last slot, 1: slot 15, 2: stream 1's first slot).  A pure function of
+// the mapping bits: compiled into constant tables for word sizes <= 8 (2^WS entries), so a
+// message reads its layout with scalar loads instead of deriving it.
+struct SlotLayout {
+    uint32_t ns, L0, k0, k1, selA[4], selB[4], edA, edB, pad[2];
+};
+template <int WS>
+struct SlotTable {
+    SlotLayout e[1 << WS];
+};
+template <int WS>
+constexpr SlotLayout make_slot_layout(uint32_t mb) {
+    SlotLayout L{};
+    uint32_t k[2] = {0, 0};
+    for (int b = 0; b < WS; ++b) k[(mb >> b) & 1u]++;
+    constexpr uint32_t WPG = 16 / WS;
+    const uint32_t L0 = WPG * k[0];
+    uint32_t sb[16] = {};
+    for (uint32_t j = 0; j < 16; ++j) {
+        const uint32_t c = j < L0 ? 0u : 1u;
+        const uint32_t jj = c ? j - L0 : j;
+        const uint32_t rank = jj % k[c];
+        uint32_t b = 0, seen = 0;
+        for (uint32_t bb = 0; bb < (uint32_t)WS; ++bb)
+            if (((mb >> bb) & 1u) == c) {
+                if (seen == rank) b = bb;
+                ++seen;
+            }
+        sb[j] = (jj / k[c]) * WS + b;
+    }
+    L.ns = k[1] ? 2u : 1u;
+    L.L0 = L0;
+    L.k0 = k[0];
+    L.k1 = k[1];
+    for (uint32_t q = 0; q < 5; ++q) {
+        uint32_t A = 0x0c0c0c0cu, B = 0x0c0c0c0cu;
+        for (uint32_t t = 0; t < 4; ++t) {
+            uint32_t sv = 0xffu;
+            if (q < 4) sv = sb[4 * t + q];
+            else if (t == 0 && L0 > 0) sv = sb[L0 - 1];
+            else if (t == 1) sv = sb[15];
+            else if (t == 2 && k[1]) sv = sb[L0];
+            if (sv == 0xffu) continue;
+            if (sv < 8) A = (A & ~(0xffu << (8 * t))) | (sv << (8 * t));
+            else B = (B & ~(0xffu << (8 * t))) | ((sv - 8) << (8 * t));
+        }
+        if (q < 4) {
+            L.selA[q] = A;
+            L.selB[q] = B;
+        } else {
+            L.edA = A;
+            L.edB = B;
+        }
+    }
+    return L;
+}
+template <int WS>
+constexpr SlotTable<WS> make_slot_table() {
+    SlotTable<WS> t{};
+    for (uint32_t mb = 0; mb < (1u << WS); ++mb) t.e[mb] = make_slot_layout<WS>(mb);
+    return t;
+}
+static __constant__ SlotTable<1> c_slots1 = make_slot_table<1>();
+static __constant__ SlotTable<2> c_slots2 = make_slot_table<2>();
+static __constant__ SlotTable<4> c_slots4 = make_slot_table<4>();
+static __constant__ SlotTable<8> c_slots8 = make_slot_table<8>();
+template <int WS>
+__device__ __forceinline__ const SlotLayout &slot_layout(uint32_t mb) {
+    if constexpr (WS == 1) return c_slots1.e[mb];
+    else if constexpr (WS == 2) return c_slots2.e[mb];
+    else if constexpr (WS == 4) return c_slots4.e[mb];
+    else return c_slots8.e[mb];
+}
 // per-wave slots (uint32, 8 per wave): 0,1 max(last run start+1); 2,3 chunk-start count;
 // 4 chunk bits of the wave's first group (combined slot layout)
 
@@ -397,15 +476,18 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
 
     // ------------------------------------------------------------ mapping (analysis)
     if constexpr (MODE == MODE_MAPPED || TL == 2 || TL == 3) {
-        uint32_t bad = 0;
+        uint32_t bad = 0, mbit = 0;
         if (lane < WS) {
             int32_t m;
             if constexpr (TL == 2 || TL == 3) m = (int32_t)((a.lmeta[lj].mapbits >> lane) & 1u);
             else m = a.mapping_in[(uint64_t)msg * WS + lane];
             bad = (m < 0 || m > 1) ? 1u : 0u;
             wm[M_MAP + lane] = (uint32_t)(m & 1);
+            mbit = (uint32_t)(m & 1);
         }
         const bool anybad = __any(bad);
+        const uint32_t mbits = (uint32_t)__ballot(mbit != 0u);  // (every wave: the same value)
+        if (lane == 0) wm[M_MAPBITS] = mbits;
         team_sync<1>();
         if (anybad) {
             // invalid caller mapping: publish an empty output for this message
@@ -477,25 +559,6 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
         const double *ltab = W == 1 ? c_log2_tab : reinterpret_cast<const double *>(smem + Lay::OFF_LOG2);
         const double *ltab2 = W == 1 ? c_log2_tab2 : ltab + 128;
         const double total = (double)wc;
-        // Counts repeat: the terms of counts 1..64 are computed once per message (exactly the
-        // operations below, so the same bits) and looked up; larger counts are computed.  Lane i
-        // holds count i + 1's terms (one-wave teams: in registers, looked up by ds_bpermute).
-        double *ctab = reinterpret_cast<double *>(smem + Lay::OFF_CTAB);
-        // (computed before the histogram: the barrier after it publishes the table)
-        double c_np = 0.0, c_L = 0.0;
-        if (TL != 1 && tid < 64) {
-            double prob;
-            {
-#pragma clang fp contract(off)
-                prob = (double)(uint32_t)(tid + 1) / total;
-                c_L = psy_log2_glibc(prob, ltab, ltab2);
-            }
-            c_np = -prob;
-            if constexpr (W > 1) {
-                ctab[2 * tid] = c_np;
-                ctab[2 * tid + 1] = c_L;
-            }
-        }
         if constexpr (TL != 4)
         for_rounds([&](uint32_t r, uint4 &d, uint32_t &, auto) __attribute__((always_inline)) {
             PSY_ASM_ROUND(H);
@@ -525,166 +588,184 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
             for (int k = 0; k < Lay::HC; ++k) c += v ? hist[b * Lay::PS + Lay::bin(v, k)] : 0u;
             return c;
         };
+        double *part = reinterpret_cast<double *>(wm + M_PART);
 
-        // entropies: calculate_entropy :470-480, TB byte positions per batch.  Each bin's
-        // (-prob, log2 prob) is computed in parallel (0, 0 for an empty bin, so the chain
-        // needs no select: fma(0, 0, e) == e for the non-negative running sum); then in every
-        // wave one lane per position runs the exact fma chain in bin order.
-        double *terms = reinterpret_cast<double *>(smem + Lay::OFF_TERMS);
-        // (-prob, log2 prob) of a bin with count c
-        auto shfl_f64 = [&](double x, uint32_t src) __attribute__((always_inline)) -> double {
-            const uint64_t u = __builtin_bit_cast(uint64_t, x);
-            const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)(uint32_t)u);
-            const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)(uint32_t)(u >> 32));
-            return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
-        };
-        auto bin_terms = [&](uint32_t c, double &np, double &L) __attribute__((always_inline)) {
-            np = 0.0;
-            L = 0.0;
-            if constexpr (W == 1) {
-                // every lane takes part in the permutes (counts 0 and > 64 read lane 0 and
-                // are then overwritten / ignored)
-                const uint32_t src = c - 1u <= 63u ? c - 1u : 0u;
-                const double tnp = shfl_f64(c_np, src), tL = shfl_f64(c_L, src);
-                if (c - 1u <= 63u) {
-                    np = tnp;
-                    L = tL;
+        // ---- Mapping decision, fast path (DESIGN.md §4 "E").  Per position b, S_b = Σ_v c_v·log2 c_v
+        // in double with the hardware log2 (v_log_f32 of (float)c: |error| <= 2^-18 for every count,
+        // checked by tests/test_gpu_0_selftest.py).  The entropy calculate_entropy :470-480 computes
+        // is e_b = log2 N - S_b/N up to the fma chain's rounding (< 5e-13), so a_b = log2 N - S_b/N
+        // differs from it by delta < 2^-18 + 2^-23 + 1e-12, and mean(a) from the reference's mean by as
+        // much.  Whenever every |a_b - mean(a)| = |S_b - mean(S)| / N exceeds kFastMargin = 1e-4 (> 2·delta)
+        // the mapping a_b > mean(a), i.e. S_b < mean(S), IS the reference's e_b > mean(e) (perform_clustering
+        // :507-525).  Otherwise — ties: constant or repeated-distribution data — the exact fma chains in
+        // bin order decide (below).  The sweep costs one log per bin and one reduction per position.
+        uint32_t exact_needed = 1;
+        if constexpr (MODE != MODE_ANALYZE) {
+            constexpr int TP = TEAM / WS;  // threads per position (4 .. 512)
+            constexpr int BPT = TP >= 256 ? 1 : 256 / TP;
+            const int pb = tid / TP, pj = tid % TP;
+            double acc = 0.0;
+#pragma unroll
+            for (int k = 0; k < BPT; ++k) {
+                const int v = pj + k * TP;
+                if (TP > 256 && v >= 256) break;  // (TEAM 512, word size 1: half the team idle)
+                const uint32_t c = count(pb, v);  // (0 for v = 0: the zero bins are summed below)
+                if (c) acc += (double)c * (double)__builtin_amdgcn_logf((float)c);
+            }
+            if constexpr (TP >= 64) {
+                acc = seg_sum_f64<64>(acc);
+                if (lane == 63) part[wv] = acc;  // wave wv: TP / 64 waves per position
+            } else {
+                acc = seg_sum_f64<TP>(acc);
+                if (pj == TP - 1) part[pb] = acc;
+            }
+            // zero bins (wave 0): LPP lanes per position, WS zero bins per lane
+            if (wv == 0) {
+                constexpr int LPP = 64 / WS;
+                const int zb = lane / LPP, zl = lane % LPP;
+                uint32_t z = 0;
+#pragma unroll
+                for (int q = 0; q < WS; ++q) z += hist[zb * Lay::PS + Lay::ZB + zl + q * LPP];
+                z = seg_sum_u32<LPP>(z);
+                if (zl == LPP - 1) wm[M_Z + zb] = z;
+            }
+            team_sync<W>();
+            if (wv == 0) {
+                double sb = 0.0;
+                if (lane < WS) {
+                    if constexpr (TP >= 64) {
+#pragma unroll
+                        for (int w = 0; w < W; ++w)
+                            if (w * 64 / TP == lane) sb += part[w];
+                    } else {
+                        sb = part[lane];
+                    }
+                    const uint32_t z = wm[M_Z + lane];
+                    if (z) sb += (double)z * (double)__builtin_amdgcn_logf((float)z);
+                }
+                double ss = 0.0;
+#pragma unroll
+                for (int b = 0; b < WS; ++b) ss += readlane_f64(sb, b);
+                const double ms = ss / (double)WS;
+                const bool unsafe = lane < WS && !(__builtin_fabs(sb - ms) > kFastMargin * total);
+                const bool fast = !__any(unsafe);
+                if (fast && lane < WS) wm[M_MAP + lane] = sb < ms ? 1u : 0u;
+                const uint32_t mbits = (uint32_t)__ballot(lane < WS && sb < ms);
+                if (lane == 0) {
+                    wm[M_EXACT] = fast ? 0u : 1u;
+                    if (fast) wm[M_MAPBITS] = mbits;
                 }
             }
-            if (c > 64u) {
+            team_sync<W>();
+            exact_needed = __builtin_amdgcn_readfirstlane(wm[M_EXACT]);
+        }
+#ifdef PSY_X_FIXMAP
+        exact_needed = 0;  // diagnostic: no entropy terms / chains
+        if (tid == 0) {
+            for (int b = 0; b < WS; ++b) wm[M_MAP + b] = b < 3 ? 1u : 0u;
+            wm[M_MAPBITS] = 7u & ((1u << WS) - 1u);
+        }
+        team_sync<W>();
+#endif
+
+        // ---- Exact path (ties, and MODE_ANALYZE's entropies): calculate_entropy :470-480 in bin
+        // order, step fma(-prob, log2 prob, e) with glibc's log2 (tdt_log2.h).  Each bin's
+        // (-prob, log2 prob) is computed in parallel (0, 0 for an empty bin, so the chain needs no
+        // select: fma(0, 0, e) == e for the non-negative running sum); then in every wave one lane
+        // per position runs the chain.
+        if (exact_needed) {
+            // Counts repeat: the terms of counts 1..64 are computed once per message (exactly the
+            // operations below, so the same bits) and looked up; larger counts are computed.  Lane i
+            // holds count i + 1's terms (one-wave teams: in registers, looked up by ds_bpermute).
+            double *ctab = reinterpret_cast<double *>(smem + Lay::OFF_CTAB);
+            double c_np = 0.0, c_L = 0.0;
+            if (tid < 64) {
                 double prob;
                 {
 #pragma clang fp contract(off)
-                    prob = (double)c / total;
-                    L = psy_log2_glibc(prob, ltab, ltab2);
+                    prob = (double)(uint32_t)(tid + 1) / total;
+                    c_L = psy_log2_glibc(prob, ltab, ltab2);
                 }
-                np = -prob;
-            } else if (W > 1 && c) {
-                const double2 t = reinterpret_cast<const double2 *>(ctab)[c - 1];
-                np = t.x;
-                L = t.y;
-            }
-        };
-        // Mapping decision fast path (DESIGN.md §4 "E").  When every position's terms fit one
-        // batch, wave 0 sums the rounded products np·L of each position in any order (16 bins per
-        // lane, then a 16-lane reduction): these approximate entropies a_b differ from the
-        // reference's fma chains e_b by at most 2·256·2^-53·8 < 5e-13 (both are sums of <= 256
-        // terms of a total <= 8 bits), the means by as much, so when every |a_b - mean(a)|
-        // exceeds kTieMargin = 1e-9 the mapping a_b > mean(a) IS the reference's e_b > mean(e).
-        // Otherwise (ties: constant or repeated-distribution data) wave 0 runs the exact chains.
-        constexpr bool ONEB = Lay::TB == WS && MODE != MODE_ANALYZE;
-        constexpr int NKB = (Lay::TB * 256 + TEAM - 1) / TEAM;  // bin batches per thread
-        double *part = reinterpret_cast<double *>(wm + M_PART);
-        auto wave_partial = [&](double x, int k) __attribute__((always_inline)) {
-            x = row_sum_f64(x);  // lane 16r + 15: row r's sum
-            const double t = readlane_f64(x, 15) + readlane_f64(x, 31) + readlane_f64(x, 47) + readlane_f64(x, 63);
-            if (lane == 0) part[k * W + wv] = t;
-        };
-        // Teams whose terms take several batches (the one-wave small-message team, word size
-        // 8/16) first run the same decision from a sweep that keeps no terms: per position,
-        // each thread sums its bins' products, one partial per (position, wave).  The batched
-        // exact path below then only runs when that sweep finds a near-tie.
-        constexpr bool SWEEP = !ONEB && MODE != MODE_ANALYZE && W * WS <= 16;
-        uint32_t nbatch = WS;  // positions the exact path covers (0: decided by the sweep)
-        if constexpr (SWEEP) {
-#pragma unroll 1
-            for (int b = 0; b < WS; ++b) {
-                double acc = 0.0;
-#pragma unroll
-                for (int k = 0; k < (256 + TEAM - 1) / TEAM; ++k) {
-                    const int v = tid + k * TEAM;
-                    if (v >= 256) break;  // wave-uniform
-                    uint32_t c = count(b, v);
-                    if (v < 64) {  // wave-uniform: bin 0 adds the 64 per-lane zero bins
-                        const uint32_t z = wave_reduce<OpAdd>(hist[b * Lay::PS + Lay::ZB + lane]);
-                        if (lane == 0) c += z;
-                    }
-                    double np, L;
-                    bin_terms(c, np, L);
-                    acc += np * L;
+                c_np = -prob;
+                if constexpr (W > 1) {
+                    ctab[2 * tid] = c_np;
+                    ctab[2 * tid + 1] = c_L;
                 }
-                wave_partial(acc, b);  // part[b·W + wv]
             }
             team_sync<W>();
-            if (wv == 0) {
-                double apl = 0.0;
-#pragma unroll
-                for (int w = 0; w < W; ++w)
-                    if (lane < WS) apl += part[lane * W + w];
-                double sa = 0.0;
-#pragma unroll
-                for (int b = 0; b < WS; ++b) sa += readlane_f64(apl, b);
-                const double ma = sa / (double)WS;
-                const bool unsafe = lane < WS && !(__builtin_fabs(apl - ma) > kTieMargin);
-                const bool fast = !__any(unsafe);
-                if (fast && lane < WS) wm[M_MAP + lane] = apl > ma ? 1u : 0u;
-                if (lane == 0) wm[M_EXACT] = fast ? 0u : 1u;
-            }
-            team_sync<W>();
-            nbatch = wm[M_EXACT] ? (uint32_t)WS : 0u;  // uniform
-        }
-#ifdef PSY_X_FIXMAP
-        nbatch = 0;  // diagnostic: no entropy terms / chains
-#endif
-        for (int q0 = 0; (uint32_t)q0 < nbatch; q0 += Lay::TB) {
-            if (q0 > 0) team_sync<W>();  // every wave's chain has read the previous batch
-            // one-wave teams keep their bins' terms in registers (no LDS terms array): bin v
-            // = 64·k + lane, read back in bin order by the chain through readlane
-            double rnp[W == 1 ? NKB : 1], rL[W == 1 ? NKB : 1];
-            {
-#pragma unroll
-            for (int k = 0; k < NKB; ++k) {
-                const int i = tid + k * TEAM;
-                if (i >= Lay::TB * 256) break;  // wave-uniform
-                const int b = q0 + i / 256;     // wave-uniform
-                double np = 0.0, L = 0.0;
-                if (b < WS) {
-                    uint32_t c = count(b, i & 255);
-                    if ((i & 255) < 64) {  // wave-uniform: bin 0 adds the 64 per-lane zero bins
-                        const uint32_t z = wave_reduce<OpAdd>(hist[b * Lay::PS + Lay::ZB + lane]);
-                        if (lane == 0) c += z;
-                    }
-                    if constexpr (MODE == MODE_ANALYZE) {
-                        if (a.hist_out) a.hist_out[((uint64_t)msg * WS + b) * 256 + (i & 255)] = c;
-                    }
-                    bin_terms(c, np, L);
-                }
+            double *terms = reinterpret_cast<double *>(smem + Lay::OFF_TERMS);
+            auto shfl_f64 = [&](double x, uint32_t src) __attribute__((always_inline)) -> double {
+                const uint64_t u = __builtin_bit_cast(uint64_t, x);
+                const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)(uint32_t)u);
+                const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)(uint32_t)(u >> 32));
+                return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+            };
+            // (-prob, log2 prob) of a bin with count c
+            auto bin_terms = [&](uint32_t c, double &np, double &L) __attribute__((always_inline)) {
+                np = 0.0;
+                L = 0.0;
                 if constexpr (W == 1) {
-                    rnp[k] = np;
-                    rL[k] = L;
-                } else {
-                    terms[2 * i] = np;
-                    terms[2 * i + 1] = L;
-                }
-                if constexpr (ONEB) wave_partial(np * L, k);
-            }
-            }
-            team_sync<W>();
-            if (wv == 0) {
-                bool exact = true;
-                if constexpr (ONEB) {
-                    // approximate entropy of position b in lane b: partial (k, w) belongs to
-                    // position (k·TEAM + 64·w) / 256
-                    double apl = 0.0;
-#pragma unroll
-                    for (int k = 0; k < NKB; ++k)
-#pragma unroll
-                        for (int w = 0; w < W; ++w)
-                            if (k * TEAM + 64 * w < Lay::TB * 256 && (k * TEAM + 64 * w) / 256 == lane)
-                                apl += part[k * W + w];
-                    double sa = 0.0;
-#pragma unroll
-                    for (int b = 0; b < WS; ++b) sa += readlane_f64(apl, b);
-                    const double ma = sa / (double)WS;
-                    const bool unsafe = lane < WS && !(__builtin_fabs(apl - ma) > kTieMargin);
-                    if (!__any(unsafe)) {
-                        exact = false;
-                        if (lane < WS) wm[M_MAP + lane] = apl > ma ? 1u : 0u;
+                    // every lane takes part in the permutes (counts 0 and > 64 read lane 0 and
+                    // are then overwritten / ignored)
+                    const uint32_t src = c - 1u <= 63u ? c - 1u : 0u;
+                    const double tnp = shfl_f64(c_np, src), tL = shfl_f64(c_L, src);
+                    if (c - 1u <= 63u) {
+                        np = tnp;
+                        L = tL;
                     }
                 }
-                if constexpr (W == 1) {
-                    static_assert(Lay::TB == 1, "one-wave teams run one position per batch");
-                    if (exact) {  // uniform: every lane runs the chain on readlane operands
+                if (c > 64u) {
+                    double prob;
+                    {
+#pragma clang fp contract(off)
+                        prob = (double)c / total;
+                        L = psy_log2_glibc(prob, ltab, ltab2);
+                    }
+                    np = -prob;
+                } else if (W > 1 && c) {
+                    const double2 t = reinterpret_cast<const double2 *>(ctab)[c - 1];
+                    np = t.x;
+                    L = t.y;
+                }
+            };
+            constexpr int NKB = (Lay::TB * 256 + TEAM - 1) / TEAM;  // bin batches per thread
+            for (int q0 = 0; q0 < WS; q0 += Lay::TB) {
+                if (q0 > 0) team_sync<W>();  // every wave's chain has read the previous batch
+                // one-wave teams keep their bins' terms in registers (no LDS terms array): bin v
+                // = 64·k + lane, read back in bin order by the chain through readlane
+                double rnp[W == 1 ? NKB : 1], rL[W == 1 ? NKB : 1];
+                {
+#pragma unroll
+                for (int k = 0; k < NKB; ++k) {
+                    const int i = tid + k * TEAM;
+                    if (i >= Lay::TB * 256) break;  // wave-uniform
+                    const int b = q0 + i / 256;     // wave-uniform
+                    double np = 0.0, L = 0.0;
+                    if (b < WS) {
+                        uint32_t c = count(b, i & 255);
+                        if ((i & 255) < 64) {  // wave-uniform: bin 0 adds the 64 per-lane zero bins
+                            const uint32_t z = wave_reduce<OpAdd>(hist[b * Lay::PS + Lay::ZB + lane]);
+                            if (lane == 0) c += z;
+                        }
+                        if constexpr (MODE == MODE_ANALYZE) {
+                            if (a.hist_out) a.hist_out[((uint64_t)msg * WS + b) * 256 + (i & 255)] = c;
+                        }
+                        bin_terms(c, np, L);
+                    }
+                    if constexpr (W == 1) {
+                        rnp[k] = np;
+                        rL[k] = L;
+                    } else {
+                        terms[2 * i] = np;
+                        terms[2 * i + 1] = L;
+                    }
+                }
+                }
+                team_sync<W>();
+                if (wv == 0) {
+                    if constexpr (W == 1) {
+                        static_assert(Lay::TB == 1, "one-wave teams run one position per batch");
+                        // uniform: every lane runs the chain on readlane operands
                         double e = 0.0;
 #pragma unroll
                         for (int k = 0; k < NKB; ++k)
@@ -692,40 +773,39 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
                             for (int l = 0; l < 64; ++l)
                                 e = __builtin_fma(readlane_f64(rnp[k], l), readlane_f64(rL[k], l), e);
                         if (lane == 0) reinterpret_cast<double *>(wm + M_ENT)[q0] = e;
+                    } else if (lane < Lay::TB && q0 + lane < WS) {
+                        const int b = q0 + lane;
+                        const double2 *tp = reinterpret_cast<const double2 *>(terms) + lane * 256;
+                        double e = 0.0;
+#pragma unroll 2
+                        for (int v = 0; v < 256; ++v) {  // (rare path: few registers, the message's are live)
+                            const double2 t = tp[v];
+                            e = __builtin_fma(t.x, t.y, e);
+                        }
+                        reinterpret_cast<double *>(wm + M_ENT)[b] = e;
                     }
-                } else if (exact && lane < Lay::TB && q0 + lane < WS) {
-                    const int b = q0 + lane;
-                    const double2 *tp = reinterpret_cast<const double2 *>(terms) + lane * 256;
-                    double e = 0.0;
-#pragma unroll 8
-                    for (int v = 0; v < 256; ++v) {
-                        const double2 t = tp[v];
-                        e = __builtin_fma(t.x, t.y, e);
-                    }
-                    reinterpret_cast<double *>(wm + M_ENT)[b] = e;
                 }
-                if (exact) wm[M_EXACT] = 1u;  // uniform in wave 0
-                else if (lane == 0) wm[M_EXACT] = 0u;
             }
-        }
-        team_sync<1>();
-        // perform_clustering :507-525 (from the exact entropies, when the chains ran)
-        if (tid == 0 && wm[M_EXACT] != 0u) {
-            const double *ent = reinterpret_cast<const double *>(wm + M_ENT);
-            double sum = 0.0;
-            for (int b = 0; b < WS; ++b) sum += ent[b];
-            double thr;
-            {
+            team_sync<1>();
+            // perform_clustering :507-525 from the exact entropies
+            if (tid == 0) {
+                const double *ent = reinterpret_cast<const double *>(wm + M_ENT);
+                double sum = 0.0;
+                for (int b = 0; b < WS; ++b) sum += ent[b];
+                double thr;
+                {
 #pragma clang fp contract(off)
-                thr = sum / (double)WS;
+                    thr = sum / (double)WS;
+                }
+                uint32_t mbits = 0;
+                for (int b = 0; b < WS; ++b) {
+                    wm[M_MAP + b] = ent[b] > thr ? 1u : 0u;
+                    mbits |= (ent[b] > thr ? 1u : 0u) << b;
+                }
+                wm[M_MAPBITS] = mbits;
             }
-            for (int b = 0; b < WS; ++b) wm[M_MAP + b] = ent[b] > thr ? 1u : 0u;
+            team_sync<W>();  // every wave reads the mapping next
         }
-#ifdef PSY_X_FIXMAP
-        if (tid == 0)
-            for (int b = 0; b < WS; ++b) wm[M_MAP + b] = b < 3 ? 1u : 0u;  // diagnostic only
-#endif
-        team_sync<1>();
         if constexpr (MODE == MODE_ANALYZE) {
             const uint64_t mb = (uint64_t)msg * WS;
             if (tid < WS) {
@@ -746,69 +826,87 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
     }
 
     if constexpr (MODE != MODE_ANALYZE) {
-        // ------------------------------------------------ slot layout (wave 0)
+        // ------------------------------------------------ slot layout
         // separate_byte_streams :527-549: slot j < L0 is stream-0 byte j of the group
         // (word j / k0, position pos0[j % k0]); slot j >= L0 is stream-1 byte j - L0.
-        // 16 lanes: slot j's source byte in the group (no per-thread arrays: scratch-free)
-        if (tid < 16) {
-            uint32_t k[2] = {0, 0};
-            for (int b = 0; b < WS; ++b) k[wm[M_MAP + b]]++;
-            const uint32_t L0 = WPG * k[0];
-            const uint32_t j = (uint32_t)lane;
-            const uint32_t c = j < L0 ? 0u : 1u;
-            const uint32_t jj = c ? j - L0 : j;
-            const uint32_t rank = jj % k[c];
-            uint32_t b = 0, seen = 0;
-            for (int bb = 0; bb < WS; ++bb) {
-                if (wm[M_MAP + bb] == c) {
-                    if (seen == rank) b = bb;
-                    ++seen;
+        uint32_t ns, L0, k0, k1, selA[4], selB[4], edA, edB;
+        const uint32_t mapbits = __builtin_amdgcn_readfirstlane(wm[M_MAPBITS]);
+        if constexpr (WS <= 8) {
+            // a constant table indexed by the mapping bits: scalar loads, no barrier
+            const SlotLayout &SL = slot_layout<WS>(mapbits);
+            ns = SL.ns;
+            L0 = SL.L0;
+            k0 = SL.k0;
+            k1 = SL.k1;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                selA[q] = SL.selA[q];
+                selB[q] = SL.selB[q];
+            }
+            edA = SL.edA;
+            edB = SL.edB;
+        } else {
+            // word size 16 (2^16 mappings): wave 0 derives it (make_slot_layout's steps), 16 lanes
+            // for slot j's source byte in the group (no per-thread arrays: scratch-free)
+            if (tid < 16) {
+                uint32_t k[2] = {0, 0};
+                for (int b = 0; b < WS; ++b) k[wm[M_MAP + b]]++;
+                const uint32_t L0w = WPG * k[0];
+                const uint32_t j = (uint32_t)lane;
+                const uint32_t c = j < L0w ? 0u : 1u;
+                const uint32_t jj = c ? j - L0w : j;
+                const uint32_t rank = jj % k[c];
+                uint32_t b = 0, seen = 0;
+                for (int bb = 0; bb < WS; ++bb) {
+                    if (wm[M_MAP + bb] == c) {
+                        if (seen == rank) b = bb;
+                        ++seen;
+                    }
+                }
+                wm[M_SB + j] = (jj / k[c]) * WS + b;
+                if (j == 0) {
+                    wm[M_NS] = k[1] ? 2u : 1u;
+                    wm[M_L0] = L0w;
+                    wm[M_K0] = k[0];
+                    wm[M_K1] = k[1];
                 }
             }
-            wm[M_SB + j] = (jj / k[c]) * WS + b;
-            if (j == 0) {
-                wm[M_NS] = k[1] ? 2u : 1u;
-                wm[M_L0] = L0;
-                wm[M_K0] = k[0];
-                wm[M_K1] = k[1];
+            team_sync<1>();
+            if (tid < 5) {
+                const uint32_t L0w = wm[M_L0];
+                const bool two = wm[M_NS] == 2;
+                uint32_t A = 0x0c0c0c0cu, B = 0x0c0c0c0cu;
+                for (int t = 0; t < 4; ++t) {
+                    // T[q] byte t = slot 4t + q; edges byte 0 stream-0 last slot, byte 1 slot 15,
+                    // byte 2 stream-1 first slot
+                    uint32_t sv = 0xffu;
+                    if (lane < 4) sv = wm[M_SB + 4 * t + lane];
+                    else if (t == 0 && L0w > 0) sv = wm[M_SB + L0w - 1];
+                    else if (t == 1) sv = wm[M_SB + 15];
+                    else if (t == 2 && two) sv = wm[M_SB + L0w];
+                    if (sv == 0xffu) continue;
+                    if (sv < 8) A = (A & ~(0xffu << (8 * t))) | (sv << (8 * t));
+                    else B = (B & ~(0xffu << (8 * t))) | ((sv - 8) << (8 * t));
+                }
+                wm[lane < 4 ? M_SELA + lane : M_EDA] = A;
+                wm[lane < 4 ? M_SELB + lane : M_EDB] = B;
             }
-        }
-        team_sync<1>();
-        if (tid < 5) {
-            const uint32_t L0 = wm[M_L0];
-            const bool two = wm[M_NS] == 2;
-            uint32_t A = 0x0c0c0c0cu, B = 0x0c0c0c0cu;
-            for (int t = 0; t < 4; ++t) {
-                // T[q] byte t = slot 4t + q; edges byte 0 stream-0 last slot, byte 1 slot 15,
-                // byte 2 stream-1 first slot
-                uint32_t s = 0xffu;
-                if (lane < 4) s = wm[M_SB + 4 * t + lane];
-                else if (t == 0 && L0 > 0) s = wm[M_SB + L0 - 1];
-                else if (t == 1) s = wm[M_SB + 15];
-                else if (t == 2 && two) s = wm[M_SB + L0];
-                if (s == 0xffu) continue;
-                if (s < 8) A = (A & ~(0xffu << (8 * t))) | (s << (8 * t));
-                else B = (B & ~(0xffu << (8 * t))) | ((s - 8) << (8 * t));
+            team_sync<W>();
+            ns = __builtin_amdgcn_readfirstlane(wm[M_NS]);
+            L0 = __builtin_amdgcn_readfirstlane(wm[M_L0]);
+            k0 = __builtin_amdgcn_readfirstlane(wm[M_K0]);
+            k1 = __builtin_amdgcn_readfirstlane(wm[M_K1]);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                selA[q] = __builtin_amdgcn_readfirstlane(wm[M_SELA + q]);
+                selB[q] = __builtin_amdgcn_readfirstlane(wm[M_SELB + q]);
             }
-            wm[lane < 4 ? M_SELA + lane : M_EDA] = A;
-            wm[lane < 4 ? M_SELB + lane : M_EDB] = B;
+            edA = __builtin_amdgcn_readfirstlane(wm[M_EDA]);
+            edB = __builtin_amdgcn_readfirstlane(wm[M_EDB]);
         }
-        team_sync<W>();
-        const uint32_t ns = __builtin_amdgcn_readfirstlane(wm[M_NS]);
         const bool ns2 = ns == 2;
-        const uint32_t L0 = __builtin_amdgcn_readfirstlane(wm[M_L0]);
-        const uint32_t k0 = __builtin_amdgcn_readfirstlane(wm[M_K0]);
-        const uint32_t k1 = __builtin_amdgcn_readfirstlane(wm[M_K1]);
         const uint32_t Ls[2] = {L0, ns2 ? 16u - L0 : 0u};
         const uint32_t lowL0 = L0 >= 16 ? 0xffffu : ((1u << L0) - 1u);
-        uint32_t selA[4], selB[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            selA[q] = __builtin_amdgcn_readfirstlane(wm[M_SELA + q]);
-            selB[q] = __builtin_amdgcn_readfirstlane(wm[M_SELB + q]);
-        }
-        const uint32_t edA = __builtin_amdgcn_readfirstlane(wm[M_EDA]);
-        const uint32_t edB = __builtin_amdgcn_readfirstlane(wm[M_EDB]);
         // selectors extracting slot L0 (stream 1's first byte) from T: slot j is byte j/4 of
         // T[j%4], i.e. byte (j%4 & 1)*4 + j/4 of perm(T[1],T[0]) or perm(T[3],T[2])
         uint32_t fsA = 0x0c0c0c0cu, fsB = 0x0c0c0c0cu;
@@ -1156,7 +1254,7 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
             else if (f == 1) v = n32;
             else if (f == 2) v = ns;
             else if (f == 3 || f == 4) v = WS;
-            else v = wm[M_MAP + (f - 5)];
+            else v = (mapbits >> (f - 5)) & 1u;
             dst[t] = (uint8_t)(v >> sh);
         }
         if (tid < 8) {
@@ -1331,15 +1429,21 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
         for (int c = 0; c < 2; ++c) pend6[c] = ((pend[c] >> 24) << 8) | ((pend[c] - 256u + gw0 * Ls[c]) & 0xffu);
         // slot 4t + q's stream position mod 256 in byte t of pos6[q] (rounds start at multiples
         // of 256 positions, so these are round-invariant)
+        // byte t of pos6[q] = ((j < L0 ? pb0 : pb1) + j) mod 256, j = 4t + q: the lane's two stream
+        // bases replicated into 4 bytes, merged by a uniform byte mask, plus the constant bytes
+        // j — a byte-wise add with no carries between bytes (low 7 bits added, bit 7 xor-ed back)
         uint32_t pos6[4] = {0, 0, 0, 0};
         if constexpr (E6) {
+            const uint32_t A4 = perm(0u, pb0, 0x00000000u), B4 = perm(0u, pb1, 0x00000000u);
 #pragma unroll
-            for (int q = 0; q < 4; ++q)
+            for (int q = 0; q < 4; ++q) {
+                uint32_t mq = 0;  // (uniform) bytes t with 4t + q < L0
 #pragma unroll
-                for (int t = 0; t < 4; ++t) {
-                    const uint32_t j = 4u * t + q;
-                    pos6[q] |= (((j < L0 ? pb0 : pb1) + j) & 0xffu) << (8 * t);
-                }
+                for (int t = 0; t < 4; ++t) mq |= (4u * t + q < L0 ? 0xffu : 0u) << (8 * t);
+                const uint32_t x = (A4 & mq) | (B4 & ~mq);
+                const uint32_t jq = 0x0c080400u + (uint32_t)q * 0x01010101u;
+                pos6[q] = ((x & 0x7f7f7f7fu) + jq) ^ (x & 0x80808080u);
+            }
         }
         auto sweep6 = [&](const uint4 &Tw, uint32_t C) __attribute__((always_inline)) {
             PSY_ASM_ROUND(B);
@@ -1450,19 +1554,31 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
 
         if constexpr (RES) {
           if constexpr (E6) {
+            // A batch of rounds is flushed when the next round could overflow a stream's staging
+            // region (capacity: the pending entry + NB rounds of 64·Ls entries), or at the
+            // wave's last round — 2 flushes for a C3 message's 8 rounds where a fixed NB = 3
+            // took 3.
+            const uint32_t cap6[2] = {1u + NB * 64u * Ls[0], 1u + NB * 64u * Ls[1]};
+            bool fresh = true;
+            uint32_t rb = 0;  // the batch's first round
 #pragma unroll
             for (int r = 0; r < G; ++r) {
                 if ((uint32_t)r < RW) {
-                    if (r % NB == 0 && lane == 0) {  // batch start: the pending entries
+                    if (fresh && lane == 0) {  // batch start: the pending entries
                         if (hp[0]) *reinterpret_cast<uint16_t *>(smem + eb6) = (uint16_t)pend6[0];
                         if (ns2 && hp[1]) *reinterpret_cast<uint16_t *>(smem + eb6 + eoff6) = (uint16_t)pend6[1];
                     }
+                    fresh = false;
 #ifndef PSY_X_NOEMIT
                     sweep6(dres[r], cres[r]);
 #endif
-                    if (r % NB == NB - 1 || (uint32_t)(r + 1) == RW) {
-                        const uint32_t gb = gw0 + (uint32_t)(r - r % NB) * 64u, ge = gw0 + (uint32_t)r * 64u + 64u;
+                    const bool over = (hp[0] ? 1u : 0u) + s6[0] + 64u * Ls[0] > cap6[0] ||
+                                      (ns2 && (hp[1] ? 1u : 0u) + s6[1] + 64u * Ls[1] > cap6[1]);
+                    if (over || (uint32_t)(r + 1) == RW) {
+                        const uint32_t gb = gw0 + rb * 64u, ge = gw0 + (uint32_t)r * 64u + 64u;
                         flush6(gb <= ngroups - 1 && ngroups - 1 < ge);
+                        fresh = true;
+                        rb = (uint32_t)r + 1u;
                     }
                 }
             }

@@ -116,3 +116,16 @@ extern "C" int selftest_log2_sweep(uint32_t N, double *d_out) {
     hipLaunchKernelGGL(log2_sweep_kernel, dim3((N + 255) / 256), dim3(256), 0, 0, N, d_out);
     return hipDeviceSynchronize() == hipSuccess ? 0 : 1;
 }
+
+// Hardware log2 (v_log_f32) of (float)c — the encode's mapping fast path (tdt_encode.h, "E")
+// bounds its error by 2^-18 per count: out[i] = log2f_hw((float)c_i) for the caller's counts.
+__global__ __launch_bounds__(256) void hw_log2_kernel(const uint32_t *c, uint32_t n, float *out) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i < n) out[i] = __builtin_amdgcn_logf((float)c[i]);
+}
+
+extern "C" int selftest_hw_log2(const uint32_t *d_c, uint32_t n, float *d_out) {
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(hw_log2_kernel, dim3((n + 255) / 256), dim3(256), 0, 0, d_c, n, d_out);
+    return hipDeviceSynchronize() == hipSuccess ? 0 : 1;
+}

@@ -112,3 +112,21 @@ def test_device_log2_sweep(N):
     # same as a rounded double multiply followed by + 0.0
     want_s = (-p) * want_l + 0.0
     assert np.array_equal(got[:, 1].view(np.uint64), want_s.view(np.uint64)), "entropy step"
+
+
+def test_hw_log2_error_bound():
+    """The encode's mapping fast path (psyne_amd/csrc/tdt_encode.h, "E") sums c·log2 c with the
+    hardware log2 of (float)c and relies on |error| <= 2^-18 for every count a message can have:
+    every c in [1, 2^24] (exact in float), and a sample of larger counts (rounded to float)."""
+    lib = C.CDLL(str(LIB))
+    lib.selftest_hw_log2.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p]
+    rng = np.random.default_rng(7)
+    cs = [np.arange(1, (1 << 24) + 1, dtype=np.uint32),
+          rng.integers(1 << 24, 1 << 32, 1 << 20, dtype=np.uint64).astype(np.uint32)]
+    for c in cs:
+        d_c = torch.from_numpy(c.astype(np.int64).astype(np.uint32).view(np.int32)).cuda()
+        out = torch.empty(c.size, dtype=torch.float32, device="cuda")
+        assert lib.selftest_hw_log2(C.c_void_p(d_c.data_ptr()), c.size, C.c_void_p(out.data_ptr())) == 0
+        got = out.cpu().numpy().astype(np.float64)
+        err = np.abs(got - np.log2(c.astype(np.float64)))
+        assert float(err.max()) <= 2.0 ** -18, "hardware log2 error %.3g > 2^-18" % float(err.max())
