@@ -157,9 +157,12 @@ struct tdt_ctx {
         uint32_t *flag = nullptr;  // pinned: the last chunk's device error flags
         uint8_t *stage_in = nullptr, *stage_out = nullptr;  // pinned staging for pageable callers
         size_t sin_bytes = 0, sout_bytes = 0;
+        hipEvent_t evc = nullptr;  // after the chunk's output copy (orders the next chunk's)
         PlanWS pw;
     } hs[2];
     std::unique_ptr<CopyPool> pool;  // host threads of the staging copies
+    uint64_t *hbases = nullptr;      // host_encode: device-side running output base per chunk
+    size_t hbases_n = 0;
     int copy_threads = 8;
     std::mutex hmu;
     // error flags of the host pipeline's chunks, OR-ed since the context was created
@@ -773,6 +776,7 @@ int ensure_slot(tdt_ctx *c, int k, size_t dev_bytes, size_t pin_words, size_t si
     if (!h.stream) {
         HIPCHK(hipStreamCreateWithFlags(&h.stream, hipStreamNonBlocking));
         HIPCHK(hipEventCreateWithFlags(&h.ev, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&h.evc, hipEventDisableTiming));
         HIPCHK(hipHostMalloc(&h.flag, 4, hipHostMallocDefault));
         *h.flag = 0;
     }
@@ -859,14 +863,61 @@ uint64_t host_decoded_size(const uint8_t *b, uint64_t len) {
     return orig;
 }
 
+// Chunk ci's compacted output → host memory, issued behind the encode kernel so that no host
+// wait sits between a chunk's kernel and its copy (the length is device-side: the chunk's last
+// offset).  dst: the slot's pinned staging (direct = 0), or the caller's pinned buffer at the
+// running base (direct = 1; bases[ci] = the totals of the chunks before, written by the previous
+// chunk's launch, which this one follows by an event).  Past out_cap nothing is copied (the host
+// reports TDT_E_CAPACITY).  Stores are 16-byte aligned on dst; the source is read as aligned
+// dwords and funnel-shifted.
+__global__ __launch_bounds__(256) void host_out_kernel(const uint8_t *src, const uint64_t *chunk_off, uint32_t n,
+                                                       uint8_t *dst, uint64_t *bases, uint32_t ci, uint64_t cap,
+                                                       int direct) {
+    const uint64_t total = chunk_off[n];
+    const uint64_t base = bases[ci];
+    if (blockIdx.x == 0 && threadIdx.x == 0) bases[ci + 1] = base + total;
+    if (base + total > cap || total == 0) return;
+    uint8_t *d = direct ? dst + base : dst;
+    const uint64_t gtid = (uint64_t)blockIdx.x * 256 + threadIdx.x, gsz = (uint64_t)gridDim.x * 256;
+    uint64_t head = (16 - ((uintptr_t)d & 15)) & 15;
+    if (head > total) head = total;
+    if (gtid < head) d[gtid] = src[gtid];
+    const uint64_t nb = (total - head) / 16;
+    const uint8_t *s0 = src + head;
+    const uint32_t sh = (uint32_t)((uintptr_t)s0 & 3) * 8;
+    const uint32_t *sw = reinterpret_cast<const uint32_t *>((uintptr_t)s0 & ~(uintptr_t)3);
+    uint4 *dv = reinterpret_cast<uint4 *>(d + head);
+    for (uint64_t k = gtid; k < nb; k += gsz) {
+        const uint32_t *q = sw + 4 * k;
+        const uint32_t w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3];
+        const uint32_t w4 = sh ? q[4] : 0u;  // (inside the chunk buffer's slack)
+        dv[k] = make_uint4((uint32_t)((((uint64_t)w1 << 32) | w0) >> sh), (uint32_t)((((uint64_t)w2 << 32) | w1) >> sh),
+                           (uint32_t)((((uint64_t)w3 << 32) | w2) >> sh), (uint32_t)((((uint64_t)w4 << 32) | w3) >> sh));
+    }
+    for (uint64_t k = head + 16 * nb + gtid; k < total; k += gsz) d[k] = src[k];
+}
+
 int host_encode(tdt_ctx *c, const uint8_t *h_in, const uint64_t *h_in_off, uint32_t n_msgs, uint8_t *h_out,
                 uint64_t out_cap, uint64_t *h_out_off, int32_t *h_status) {
     const int ws = c->cfg.word_size;
-    const bool pin_in = is_pinned(h_in + h_in_off[0]), pin_out = is_pinned(h_out);
+    const bool pin_in = is_pinned(h_in + h_in_off[0]);
+    // a pinned caller buffer receives the chunks' output straight from the copy kernels
+    uint8_t *d_out = nullptr;
+    if (is_pinned(h_out) && hipHostGetDevicePointer(reinterpret_cast<void **>(&d_out), h_out, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        d_out = nullptr;
+    }
+    const bool pin_out = d_out != nullptr;
     std::vector<Chunk> ch;
     for (uint32_t m = 0; m < n_msgs;) {
         ch.push_back(plan_chunk(h_in_off, m, n_msgs, true, ws, nullptr));
         m += ch.back().n;
+    }
+    if (ch.size() + 1 > c->hbases_n) {
+        if (c->hbases) HIPCHK(hipFree(c->hbases));
+        c->hbases = nullptr;
+        HIPCHK(hipMalloc(&c->hbases, 8 * (ch.size() + 1)));
+        c->hbases_n = ch.size() + 1;
     }
     uint64_t base = 0;  // output bytes of the chunks finished so far
     bool capacity = false;
@@ -895,6 +946,14 @@ int host_encode(tdt_ctx *c, const uint8_t *h_in, const uint64_t *h_in_off, uint3
         st = encode_common(c, psy::MODE_ENCODE, d, doff, k.n, nullptr, d + k.o_out, k.cap, dooff, dst, nullptr, nullptr,
                            nullptr, h.stream, nullptr, nullptr, d + k.o_ws);
         if (st) return st;
+        // the output, in chunk order (each copy follows the previous chunk's: the running base)
+        if (ci == 0) HIPCHK(hipMemsetAsync(c->hbases, 0, 8, h.stream));
+        else HIPCHK(hipStreamWaitEvent(h.stream, c->hs[(ci - 1) & 1].evc, 0));
+        const uint32_t grid = (uint32_t)std::min<uint64_t>(1024, k.cap / 4096 + 1);
+        hipLaunchKernelGGL(host_out_kernel, dim3(grid), dim3(256), 0, h.stream, d + k.o_out, dooff, k.n,
+                           pin_out ? d_out : h.stage_out, c->hbases, (uint32_t)ci, out_cap, pin_out ? 1 : 0);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(h.evc, h.stream));
         HIPCHK(hipMemcpyAsync(h.flag, d + k.o_ws + 4, 4, hipMemcpyDeviceToHost, h.stream));
         HIPCHK(hipMemcpyAsync(h.pin + (k.n + 1), dooff, 8ull * (k.n + 1), hipMemcpyDeviceToHost, h.stream));
         HIPCHK(hipMemcpyAsync(h.pin + 3ull * k.n + 2, dst, 4ull * k.n, hipMemcpyDeviceToHost, h.stream));
@@ -911,15 +970,8 @@ int host_encode(tdt_ctx *c, const uint8_t *h_in, const uint64_t *h_in_off, uint3
         if (capacity || base + total > out_cap) capacity = true;
         for (uint32_t i = 0; i < k.n; ++i) h_out_off[k.m0 + i] = base + (capacity ? 0 : pin_out_off[i]);
         if (h_status) std::memcpy(h_status + k.m0, h.pin + 3ull * k.n + 2, 4ull * k.n);
-        if (!capacity && total) {
-            if (pin_out) {
-                HIPCHK(hipMemcpyAsync(h_out + base, h.dev + k.o_out, total, hipMemcpyDeviceToHost, h.stream));
-            } else {
-                HIPCHK(hipMemcpyAsync(h.stage_out, h.dev + k.o_out, total, hipMemcpyDeviceToHost, h.stream));
-                HIPCHK(hipStreamSynchronize(h.stream));
-                c->pool->copy(h_out + base, h.stage_out, total);
-            }
-        }
+        // (the copy kernel has written the output: into h_out directly, or into the staging)
+        if (!capacity && total && !pin_out) c->pool->copy(h_out + base, h.stage_out, total);
         if (!capacity) base += total;
         return TDT_OK;
     };
@@ -1169,6 +1221,7 @@ void tdt_ctx_destroy(tdt_ctx *ctx) {
     if (ctx->cp_buf) (void)hipFree(ctx->cp_buf);
     if (ctx->cp_idx) (void)hipFree(ctx->cp_idx);
     ctx->pw.release();
+    if (ctx->hbases) (void)hipFree(ctx->hbases);
     if (ctx->astream) (void)hipStreamSynchronize(ctx->astream);
     if (ctx->h_dev) (void)hipFree(ctx->h_dev);
     if (ctx->astream) (void)hipStreamDestroy(ctx->astream);
@@ -1181,6 +1234,7 @@ void tdt_ctx_destroy(tdt_ctx *ctx) {
         if (h.stage_out) (void)hipHostFree(h.stage_out);
         h.pw.release();
         if (h.ev) (void)hipEventDestroy(h.ev);
+        if (h.evc) (void)hipEventDestroy(h.evc);
         if (h.stream) (void)hipStreamDestroy(h.stream);
     }
     delete ctx;

@@ -16,6 +16,40 @@
 #include <thread>
 #include <vector>
 
+#if defined(__x86_64__) && !defined(__HIP_DEVICE_COMPILE__)
+#include <immintrin.h>
+// Large copies into the pinned staging (and out of it into the caller's buffer) stream past
+// the caches: 32-byte non-temporal stores, no read-for-ownership of the destination.
+__attribute__((target("avx2"))) inline void nt_copy_avx2(uint8_t *d, const uint8_t *s, size_t n) {
+    size_t head = (32 - ((uintptr_t)d & 31)) & 31;
+    if (head > n) head = n;
+    std::memcpy(d, s, head);
+    d += head;
+    s += head;
+    n -= head;
+    size_t i = 0;
+    for (; i + 128 <= n; i += 128) {
+        const __m256i a = _mm256_loadu_si256(reinterpret_cast<const __m256i *>(s + i));
+        const __m256i b = _mm256_loadu_si256(reinterpret_cast<const __m256i *>(s + i + 32));
+        const __m256i c = _mm256_loadu_si256(reinterpret_cast<const __m256i *>(s + i + 64));
+        const __m256i e = _mm256_loadu_si256(reinterpret_cast<const __m256i *>(s + i + 96));
+        _mm256_stream_si256(reinterpret_cast<__m256i *>(d + i), a);
+        _mm256_stream_si256(reinterpret_cast<__m256i *>(d + i + 32), b);
+        _mm256_stream_si256(reinterpret_cast<__m256i *>(d + i + 64), c);
+        _mm256_stream_si256(reinterpret_cast<__m256i *>(d + i + 96), e);
+    }
+    std::memcpy(d + i, s + i, n - i);
+    _mm_sfence();
+}
+inline void part_copy(uint8_t *d, const uint8_t *s, size_t n) {
+    static const bool avx2 = __builtin_cpu_supports("avx2");
+    if (avx2) nt_copy_avx2(d, s, n);
+    else std::memcpy(d, s, n);
+}
+#else
+inline void part_copy(uint8_t *d, const uint8_t *s, size_t n) { std::memcpy(d, s, n); }
+#endif
+
 class CopyPool {
   public:
     explicit CopyPool(int threads) {
@@ -73,7 +107,7 @@ class CopyPool {
             const size_t i = j.next.fetch_add(1);
             if (i >= j.parts) return;
             const size_t b = i * per, e = std::min(j.bytes, b + per);
-            if (b < e) std::memcpy(j.d + b, j.s + b, e - b);
+            if (b < e) part_copy(j.d + b, j.s + b, e - b);
             if (j.left.fetch_sub(1) == 1) {
                 std::lock_guard<std::mutex> lk(m_);
                 done_.notify_all();

@@ -530,9 +530,11 @@ def test_slot_offsets_multi_chunk(n):
 
 def test_mapping_ties_exact_fallback(orc):
     """Messages whose byte-position entropies tie (or nearly tie) with their mean: the
-    kernel's any-order entropy sums cannot decide them (kTieMargin), so it must fall back to
-    the reference's sequential fma chains (tdt_compression.hpp:470-480) — compared here with
-    the oracle byte for byte, for the 512-lane (64 KiB) and the one-wave (1-4 KiB) teams."""
+    kernel's hardware-log2 entropy sums cannot decide them (|a_b - mean| <= kFastMargin), so it
+    must fall back to the reference's sequential fma chains (tdt_compression.hpp:470-480) —
+    compared here with the oracle byte for byte, for the 512-lane (64 KiB) and the one-wave
+    (1-4 KiB) teams.  The near ties (a copied position with k samples changed) straddle the
+    margin: some messages take the fast decision, some the exact one."""
     rng = np.random.default_rng(41)
     msgs = []
     for n in (1024, 4096, 65536):
@@ -548,5 +550,12 @@ def test_mapping_ties_exact_fallback(orc):
         msgs.append(z)
         g = grad(rng, w)
         msgs.append(g)
+        for k in (1, 2, 3, 5, 9, 17):                                  # near ties around the margin
+            y = rng.integers(0, 256, (w, 4), dtype=np.uint8)
+            y[:, 1] = y[:, 0]
+            idx = rng.choice(w, k, replace=False)
+            y[idx, 1] = rng.integers(0, 256, k, dtype=np.uint8)
+            y[:, 3] = np.roll(y[:, 2], 3)
+            msgs.append(y.reshape(-1))
     check_vs_oracle(orc, make_codec(), msgs)
     check_vs_oracle(orc, make_codec(hint=1024), msgs)
