@@ -477,6 +477,58 @@ __device__ __forceinline__ void decode_fast(const FastHdr &H, uint8_t *smem, con
     }
 }
 
+// Recombine layout of a blob with at most two streams, word size <= 8, as a function of its
+// mapping bits (bit b = mapping[b] in {0, 1}): the referenced stream of first use (r = 0) holds
+// mapping[0]'s value; two = both values occur; seg[r] = bytes of stream r per 16-byte group;
+// OA / OB = the v_perm selectors that scatter a group's S dwords (its seg[0] bytes of stream
+// r = 0, then its seg[1] bytes of stream r = 1) into word order (recombine :614-637): output
+// byte i = word i / ws, position b = i % ws → S byte (r_b ? seg0 : 0) + (i / ws)·k_b + rank_b.
+// Compiled into constant tables (parse_fast's general derivation handles everything else).
+struct RecLayout {
+    uint32_t two, m0, seg0, seg1, OA[4], OB[4];
+};
+template <int WS>
+struct RecTable {
+    RecLayout e[1 << WS];
+};
+template <int WS>
+constexpr RecLayout make_rec_layout(uint32_t mb) {
+    RecLayout L{};
+    constexpr uint32_t WPG = 16 / WS;
+    const uint32_t m0 = mb & 1u;
+    uint32_t k[2] = {0, 0};
+    for (int b = 0; b < WS; ++b) k[(mb >> b) & 1u]++;
+    L.m0 = m0;
+    L.two = (k[0] && k[1]) ? 1u : 0u;
+    L.seg0 = WPG * k[m0];
+    L.seg1 = L.two ? WPG * k[m0 ^ 1u] : 0u;
+    uint32_t A[4] = {0x0c0c0c0cu, 0x0c0c0c0cu, 0x0c0c0c0cu, 0x0c0c0c0cu}, B[4] = {0x0c0c0c0cu, 0x0c0c0c0cu, 0x0c0c0c0cu, 0x0c0c0c0cu};
+    for (uint32_t i = 0; i < 16; ++i) {
+        const uint32_t b = i % WS, v = (mb >> b) & 1u;
+        uint32_t rank = 0;
+        for (uint32_t bb = 0; bb < b; ++bb) rank += ((mb >> bb) & 1u) == v ? 1u : 0u;
+        const uint32_t sidx = (v == m0 ? 0u : L.seg0) + (i / WS) * k[v] + rank;
+        const uint32_t q = i >> 2, sh = 8u * (i & 3u);
+        if (sidx < 8) A[q] = (A[q] & ~(0xffu << sh)) | (sidx << sh);
+        else B[q] = (B[q] & ~(0xffu << sh)) | ((sidx - 8) << sh);
+    }
+    for (int q = 0; q < 4; ++q) {
+        L.OA[q] = A[q];
+        L.OB[q] = B[q];
+    }
+    return L;
+}
+template <int WS>
+constexpr RecTable<WS> make_rec_table() {
+    RecTable<WS> t{};
+    for (uint32_t mb = 0; mb < (1u << WS); ++mb) t.e[mb] = make_rec_layout<WS>(mb);
+    return t;
+}
+static __constant__ RecTable<1> c_rec1 = make_rec_table<1>();
+static __constant__ RecTable<2> c_rec2 = make_rec_table<2>();
+static __constant__ RecTable<4> c_rec4 = make_rec_table<4>();
+static __constant__ RecTable<8> c_rec8 = make_rec_table<8>();
+
 // Wave-parallel header parse (decode :271-304, deserialize :119-170, recombine :614-637) for
 // the blobs the fast path takes: UNCP, or a valid TDT blob with word size 1/2/4/8/16, at most
 // 16 streams, a mapping inside the header cache, at most two referenced streams whose
@@ -499,6 +551,47 @@ __device__ __forceinline__ FastHdr parse_fast(const uint8_t *blob, uint64_t len,
     const uint32_t orig = hw(4), ns = hw(8), ws = hw(12), msize = hw(16);
     if (!(ws == 1 || ws == 2 || ws == 4 || ws == 8 || ws == 16) || msize < ws || ns == 0 || ns > 16) return h;
     if (20u + 4u * msize + 4u > hcl || orig / ws == 0) return h;
+    if (ns <= 2 && ws <= 8) {
+        // one or two streams, word size <= 8 (every blob the encoder writes for ws <= 8): the
+        // stream table is two length words, the recombine layout a table entry
+        const uint32_t m = lane < ws ? hw(20 + 4 * lane) : 0u;
+        if (__any(lane < ws && m >= ns)) return h;  // (also negative values) → BAD_MAPPING via blob_check
+        const uint32_t mb = (uint32_t)__ballot(lane < ws && m == 1u);
+        uint64_t off = 20ull + 4ull * msize;
+        if (off + 4 > len) return h;
+        const uint32_t l0 = hw((uint32_t)off);  // (off + 4 <= hcl, off % 4 == 0)
+        const uint32_t o0 = (uint32_t)off + 4u;
+        if ((uint64_t)o0 + l0 > len) return h;
+        uint32_t o1 = 0, l1 = 0;
+        if (ns == 2) {
+            const uint64_t t1 = (uint64_t)o0 + l0;
+            if (t1 + 4 > len) return h;
+            l1 = t1 + 4 <= hcl ? ld_u32_bytes(hdr + t1) : ld_u32_bytes(blob + t1);
+            o1 = (uint32_t)t1 + 4u;
+            if ((uint64_t)o1 + l1 > len) return h;
+        }
+        const RecLayout &R = ws == 1 ? c_rec1.e[mb] : ws == 2 ? c_rec2.e[mb] : ws == 4 ? c_rec4.e[mb] : c_rec8.e[mb];
+        const uint32_t seg0 = R.seg0, seg1 = R.seg1;
+        if ((seg0 & 3u) || (seg1 & 3u)) return h;
+        const bool first1 = R.m0 != 0;  // stream 1 is used first: it is r = 0
+        h.soff[0] = first1 ? o1 : o0;
+        h.np[0] = (first1 ? l1 : l0) / 2u;
+        h.soff[1] = R.two ? (first1 ? o0 : o1) : 0u;
+        h.np[1] = R.two ? (first1 ? l0 : l1) / 2u : 0u;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            h.OA[q] = R.OA[q];
+            h.OB[q] = R.OB[q];
+        }
+        h.orig = orig;
+        h.ws = ws;
+        h.two = R.two;
+        h.seg[0] = seg0;
+        h.seg[1] = seg1;
+        h.osize = orig;
+        h.kind = 2;
+        return h;
+    }
     // stream table: lane s keeps stream s's data offset and length
     uint64_t off = 20ull + 4ull * msize;
     uint32_t my_off = 0, my_len = 0;
