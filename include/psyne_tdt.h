@@ -98,9 +98,12 @@ void tdt_ctx_destroy(tdt_ctx *ctx);
 void tdt_ctx_set_metrics(tdt_ctx *ctx, double bandwidth_mbps, double latency_ms, double cpu_usage);
 void tdt_ctx_get_metrics(const tdt_ctx *ctx, double *bandwidth_mbps, double *latency_ms, double *cpu_usage);
 
-/* Hint of the typical message size in bytes: selects the encode team shape (one 64-lane wave
- * per message up to 4 KiB, a 512-lane workgroup otherwise).  Optional; any size encodes
- * correctly with either shape. */
+/* Seed for the team shape of one-pass launches whose message sizes the host does not know
+ * (tdt_encode_with_mapping_batch, tdt_analyze_batch, and tdt_encode_batch under stream
+ * capture): one 64-lane wave per message up to 4 KiB, a 512-lane workgroup otherwise.  Once a
+ * slotted plan of this context has completed, its class counts decide instead; the slotted
+ * calls, tdt_encode_batch outside capture and the host pipeline never use it.  Optional; any
+ * size encodes correctly with either shape. */
 void tdt_ctx_set_size_hint(tdt_ctx *ctx, uint64_t typical_message_bytes);
 
 /* should_transform (:186-201) for a message of n bytes under the current metrics. */

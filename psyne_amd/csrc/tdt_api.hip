@@ -77,10 +77,12 @@ struct CountHist {
     hipEvent_t ev = nullptr;
     bool pending = false, valid = false;
     uint32_t v[16] = {};
+    uint32_t n = 0, n_pending = 0;  // messages in the snapshot's batch
     // fold the newest completed snapshot in (never waits)
     void refresh() {
         if (pending && hipEventQuery(ev) == hipSuccess) {
             std::memcpy(v, pin, sizeof(v));
+            n = n_pending;
             valid = true;
             pending = false;
         }
@@ -263,13 +265,14 @@ int ensure_plan(PlanWS &w, uint32_t n, hipStream_t s) {
 }
 
 // The plan counters of this call → pinned snapshot (not under stream capture).
-int record_counts(CountHist &h, const void *dcnt, hipStream_t s) {
+int record_counts(CountHist &h, const void *dcnt, uint32_t n_msgs, hipStream_t s) {
     if (!h.pin) {
         HIPCHK(hipHostMalloc(&h.pin, 64, hipHostMallocDefault));
         HIPCHK(hipEventCreateWithFlags(&h.ev, hipEventDisableTiming));
     }
     HIPCHK(hipMemcpyAsync(h.pin, dcnt, 64, hipMemcpyDeviceToHost, s));
     HIPCHK(hipEventRecord(h.ev, s));
+    h.n_pending = n_msgs;
     h.pending = true;
     return TDT_OK;
 }
@@ -377,7 +380,7 @@ int launch_slotted(tdt_ctx *c, PlanWS &pw, psy::EncodeArgs a, hipStream_t s) {
     hipLaunchKernelGGL(psy::tdt_encode_plan_kernel, dim3((uint32_t)(((uint64_t)n + per - 1) / per)),
                        dim3(psy::kPlanThreads), 0, s, p);
     HIPCHK(hipGetLastError());
-    if (!capturing && (st = record_counts(H, cnt, s))) return st;
+    if (!capturing && (st = record_counts(H, cnt, n, s))) return st;
     a.pcnt = cnt;
     const uint32_t ovf512 = (uint32_t)c->cus * 3, ovf64 = (uint32_t)c->cus * 24;
     // main launch over [0, g) + overflow launch over [g, count) of one class
@@ -487,9 +490,19 @@ int launch_encode_ws(psy::EncodeArgs a, bool small, hipStream_t s) {
 }
 
 // LB: compacted output (look-back) vs slotted output
+// Team shape of a one-pass (look-back) launch when the caller does not know the batch's sizes:
+// one-wave teams when most messages of this context's latest slotted plan were small (<= 4 KiB),
+// the size hint only before any plan has been observed.
+bool lb_small_teams(tdt_ctx *c, hipStream_t s) {
+    CountHist &H = c->pw.eh;
+    if (!capturing(s)) H.refresh();
+    if (H.valid && H.n) return 2ull * H.v[10] > H.n;  // (counter 5: small messages)
+    return c->size_hint.load() <= kSmallMax;
+}
+
 template <int MODE, int LB>
-int launch_encode(tdt_ctx *c, psy::EncodeArgs a, hipStream_t s) {
-    const bool small = c->size_hint.load() <= 4096;
+int launch_encode(tdt_ctx *c, psy::EncodeArgs a, hipStream_t s, int small_teams) {
+    const bool small = small_teams < 0 ? lb_small_teams(c, s) : small_teams != 0;
     switch (c->cfg.word_size) {
 #ifdef PSY_FAST_BUILD  // diagnostic builds: word_size 4 only
         case 4: return launch_encode_ws<4, MODE, LB>(a, small, s);
@@ -530,7 +543,7 @@ int encode_common(tdt_ctx *c, int mode, const uint8_t *d_in, const uint64_t *d_i
                   const int32_t *d_mapping, uint8_t *d_out, uint64_t out_cap, uint64_t *d_out_off,
                   int32_t *d_status, uint32_t *d_hist, double *d_ent, int32_t *d_map, void *stream,
                   const uint64_t *d_slot_off = nullptr, uint64_t *d_out_len = nullptr, uint8_t *wsp = nullptr,
-                  PlanWS *pws = nullptr) {
+                  PlanWS *pws = nullptr, int small_teams = -1) {
     if (!c) return set_err(TDT_E_ARG, "null context");
     if (n_msgs == 0) return TDT_OK;
     if (!d_in_off) return set_err(TDT_E_ARG, "null input offsets");  // d_in may be null: all-empty batch
@@ -562,11 +575,12 @@ int encode_common(tdt_ctx *c, int mode, const uint8_t *d_in, const uint64_t *d_i
     a.slot_off = d_slot_off;
     a.out_len = d_out_len;
     if (mode == psy::MODE_ENCODE) {
-        st = slotted ? launch_slotted_any(c, pws ? *pws : c->pw, a, s) : launch_encode<psy::MODE_ENCODE, 1>(c, a, s);
+        st = slotted ? launch_slotted_any(c, pws ? *pws : c->pw, a, s)
+                     : launch_encode<psy::MODE_ENCODE, 1>(c, a, s, small_teams);
     } else if (mode == psy::MODE_MAPPED) {
-        st = launch_encode<psy::MODE_MAPPED, 1>(c, a, s);
+        st = launch_encode<psy::MODE_MAPPED, 1>(c, a, s, small_teams);
     } else {
-        st = launch_encode<psy::MODE_ANALYZE, 1>(c, a, s);
+        st = launch_encode<psy::MODE_ANALYZE, 1>(c, a, s, small_teams);
     }
     if (st) return st;
     HIPCHK(hipGetLastError());
@@ -635,7 +649,7 @@ int launch_decode_slotted(tdt_ctx *c, PlanWS &pw, psy::DecodeArgs a, hipStream_t
                      lcap, bcap, tcap, c->large_min, small_on ? 1u : 0u};
     hipLaunchKernelGGL(psy::tdt_decode_plan_kernel, dim3((uint32_t)(((uint64_t)n + 4095) / 4096)), dim3(1024), 0, s, p);
     HIPCHK(hipGetLastError());
-    if (!capturing && (st = record_counts(H, cnt, s))) return st;
+    if (!capturing && (st = record_counts(H, cnt, n, s))) return st;
     a.dmeta = dmeta;
     a.bent = bent;
     a.bsum = bsum;
@@ -944,7 +958,8 @@ int host_encode(tdt_ctx *c, const uint8_t *h_in, const uint64_t *h_in_off, uint3
         HIPCHK(hipMemcpyAsync(d, src, k.in_bytes, hipMemcpyHostToDevice, h.stream));
         HIPCHK(hipMemcpyAsync(doff, pin_in_off, 8ull * (k.n + 1), hipMemcpyHostToDevice, h.stream));
         st = encode_common(c, psy::MODE_ENCODE, d, doff, k.n, nullptr, d + k.o_out, k.cap, dooff, dst, nullptr, nullptr,
-                           nullptr, h.stream, nullptr, nullptr, d + k.o_ws);
+                           nullptr, h.stream, nullptr, nullptr, d + k.o_ws, nullptr,
+                           k.in_bytes <= kSmallMax * k.n ? 1 : 0);  // (the chunk's sizes are host data)
         if (st) return st;
         // the output, in chunk order (each copy follows the previous chunk's: the running base)
         if (ci == 0) HIPCHK(hipMemsetAsync(c->hbases, 0, 8, h.stream));
@@ -1323,9 +1338,9 @@ int tdt_encode_batch(tdt_ctx *ctx, const uint8_t *d_in, const uint64_t *d_in_off
     // one pass with the look-back for batches of medium messages (all <= 64 KiB, 16 KiB or more
     // on average); small messages make the per-message ticket and look-back chain the limit
     // (C2: 12 ms for 1 Mi x 1 KiB), long ones stall it — both take the two phases
-    if (!h3[0] && (h3[2] - h3[1]) >= 16384ull * n_msgs)
+    if (!h3[0] && (h3[2] - h3[1]) >= 16384ull * n_msgs)  // (16 KiB on average: 512-lane teams)
         return encode_common(ctx, psy::MODE_ENCODE, d_in, d_in_off, n_msgs, nullptr, d_out, out_cap, d_out_off,
-                             d_status, nullptr, nullptr, nullptr, stream);
+                             d_status, nullptr, nullptr, nullptr, stream, nullptr, nullptr, nullptr, nullptr, 0);
     uint64_t *slot = ctx->cp_idx, *len = ctx->cp_idx + n_msgs + 1;
     // Σ encode bounds <= 2·(input bytes) + n·(28 + 4·ws) (and >= n + 4 per message)
     const uint64_t bound = 2 * (h3[2] - h3[1]) + (uint64_t)n_msgs * (28 + 4ull * (uint64_t)ctx->cfg.word_size + 4);
@@ -1499,7 +1514,8 @@ int tdt_analyze_host(tdt_ctx *ctx, const uint8_t *h_in, const uint64_t *h_in_off
     HIPCHK(hipMemcpyAsync(d + o_off, tmp.data(), 8ull * (n_msgs + 1), hipMemcpyHostToDevice, s));
     st = encode_common(ctx, psy::MODE_ANALYZE, d, reinterpret_cast<uint64_t *>(d + o_off), n_msgs, nullptr, nullptr,
                        0, nullptr, reinterpret_cast<int32_t *>(d + o_st), nullptr,
-                       reinterpret_cast<double *>(d + o_ent), reinterpret_cast<int32_t *>(d + o_map), s);
+                       reinterpret_cast<double *>(d + o_ent), reinterpret_cast<int32_t *>(d + o_map), s, nullptr,
+                       nullptr, nullptr, nullptr, in_bytes <= kSmallMax * n_msgs ? 1 : 0);
     if (st) return st;
     if (h_entropy) HIPCHK(hipMemcpyAsync(h_entropy, d + o_ent, 8ull * n_msgs * ws, hipMemcpyDeviceToHost, s));
     if (h_mapping) HIPCHK(hipMemcpyAsync(h_mapping, d + o_map, 4ull * n_msgs * ws, hipMemcpyDeviceToHost, s));

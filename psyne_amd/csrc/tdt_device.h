@@ -340,6 +340,14 @@ __device__ __forceinline__ uint64_t lookback_excl(uint64_t *st, uint32_t i, uint
     return excl;
 }
 
+// A u64 made wave-uniform (lane 0's).  readfirstlane returns int: each half goes through
+// uint32_t, or a low half >= 2^31 would sign-extend over the high one.
+__device__ __forceinline__ uint64_t rfl_u64(uint64_t v) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
 // Sum of a u64 over the wave (butterfly on both 32-bit halves).
 __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 #pragma unroll
@@ -356,6 +364,12 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 // words below the window's top at once; the nearest inclusive prefix (a ballot) ends the
 // walk, windows of aggregates are summed and skipped, a window with an unpublished word is
 // re-read.  Message indices below 0 read as "inclusive 0".  Bounded spin as above.
+// Split form of lookback_excl_wave for a team that publishes its aggregate early and needs
+// its exclusive prefix only later: lookback_publish (wave 0 of the team), then
+// lookback_resolve (the same wave) returns the prefix and publishes the inclusive value.
+__device__ __forceinline__ void lookback_publish(uint64_t *st, uint32_t i, uint64_t agg);
+__device__ __forceinline__ uint64_t lookback_resolve(uint64_t *st, uint32_t i, uint64_t agg, uint32_t *timeout);
+
 __device__ __forceinline__ uint64_t lookback_excl_wave(uint64_t *st, uint32_t i, uint64_t agg,
                                                        uint32_t *timeout) {
     const int lane = lane_id();
@@ -405,6 +419,38 @@ __device__ __forceinline__ uint64_t lookback_excl_wave(uint64_t *st, uint32_t i,
         if (spins) atomicAdd(&psy_prof[19], 1ull);
     }
 #endif
+    return excl;
+}
+
+__device__ __forceinline__ void lookback_publish(uint64_t *st, uint32_t i, uint64_t agg) {
+    if (lane_id() == 0) lb_store(&st[i], (i == 0 ? kLbInc : kLbAgg) | agg);
+}
+__device__ __forceinline__ uint64_t lookback_resolve(uint64_t *st, uint32_t i, uint64_t agg, uint32_t *timeout) {
+    const int lane = lane_id();
+    if (i == 0) return 0;
+    uint64_t excl = 0;
+    int64_t top = (int64_t)i;  // window [top - 64, top)
+    uint32_t spins = 0;
+    while (true) {
+        const int64_t j = top - 64 + lane;
+        const uint64_t s = j >= 0 ? lb_load(&st[j]) : kLbInc;
+        const uint32_t f = (uint32_t)(s >> 62);
+        const uint64_t bz = __ballot(f == 0);
+        const uint64_t bp = __ballot(f == 2);
+        const uint64_t need = bp ? ~0ull << (63 - __builtin_clzll(bp)) : ~0ull;
+        if (bz & need) {
+            if (++spins > (1u << 24)) {
+                if (lane == 0) atomicOr(timeout, 1u);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        excl += wave_sum_u64(((need >> lane) & 1ull) ? (s & kLbVal) : 0ull);
+        if (bp) break;
+        top -= 64;
+    }
+    if (lane == 0) lb_store(&st[i], kLbInc | (excl + agg));
     return excl;
 }
 

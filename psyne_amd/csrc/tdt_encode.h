@@ -174,7 +174,7 @@ enum {
     M_MSG = 0, M_NS = 1, M_L0 = 2, M_K0 = 3, M_K1 = 4, M_SELA = 8 /*4*/, M_SELB = 12 /*4*/, M_EDA = 16,
     M_EDB = 17, M_EXACT = 18, M_STATUS = 26, M_MAP = 32 /*16*/, M_ENT = 64 /*16 doubles*/, M_BASE = 96 /*u64*/,
     M_SB = 100 /*16*/, M_PART = 128 /*16 doubles: per-wave entropy partials*/, M_Z = 48 /*16: zero-bin totals*/,
-    M_MAPBITS = 5 /*bit b = mapping[b]*/
+    M_MAPBITS = 5 /*bit b = mapping[b]*/, M_READY = 6 /*deferred look-back: offset published*/
 };
 // decision margin of the mapping fast path, in bits of entropy (> 2x its worst-case error)
 constexpr double kFastMargin = 1e-4;
@@ -332,7 +332,11 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
         uint64_t ob;
         if constexpr (LB) {
             if (wv == 0) {
+#ifndef PSY_X_NOLB
                 const uint64_t b = lookback_excl_wave(a.lookback, msg, E, a.errflags);
+#else
+                const uint64_t b = (uint64_t)msg * (28 + 4 * WS + 2ull * n);  // diagnostic: no look-back
+#endif
                 if (lane == 0) *reinterpret_cast<uint64_t *>(misc + M_BASE) = b;
             }
             team_sync<W>();
@@ -503,6 +507,7 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
         // lanes to the same address when they hold the same nonzero value.
         uint32_t *hist = reinterpret_cast<uint32_t *>(smem + Lay::OFF_HIST);
         for (int i = tid; i < WS * Lay::PS / 4; i += TEAM) reinterpret_cast<uint4 *>(hist)[i] = make_uint4(0, 0, 0, 0);
+        if (tid == 0) wm[M_READY] = 0u;  // (published by the barrier below)
         if constexpr (TL == 4) {
             // the message's histogram: the sum of its span histograms, into copy 0 of the bins
             team_sync<W>();
@@ -1229,6 +1234,9 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
         const uint32_t hdr = 20 + 4 * WS;
         uint64_t ob;
         uint32_t P0m = P0;  // stream 0's pair count in the whole message
+        uint64_t Eblob = 0;
+        // deferred look-back: compacted output of a resident message (the E6 emit below)
+        constexpr bool DEFER = LB && RES && WS <= 4 && TL == 0 && MODE == MODE_ENCODE;
         if constexpr (TL == 3) {
             const LMeta *lm = a.lmeta + lj;
             if (!lm->fits) return;  // the scan gave the message CAPACITY
@@ -1238,15 +1246,24 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
             pin[1] += tr->cnt[1];
         } else {
             const uint64_t E = hdr + (4 + 2ull * P0) + (ns2 ? 4 + 2ull * P1 : 0);
-            bool fits;
-            ob = place(E, fits);
-            if (tid == 0 && a.status) a.status[msg] = fits ? ST_OK : ST_CAPACITY;
-            if (!fits) return;
+            Eblob = E;
+            bool fits = true;
+            if constexpr (DEFER) {
+                // compacted, resident: publish the blob size now and take the offset only at the
+                // first flush (pass B's sweeps fill the LDS staging meanwhile), so the wait for
+                // the predecessors' prefixes overlaps this team's own work
+                if (wv == 0) lookback_publish(a.lookback, msg, E);
+                ob = 0;
+            } else {
+                ob = place(E, fits);
+                if (tid == 0 && a.status) a.status[msg] = fits ? ST_OK : ST_CAPACITY;
+                if (!fits) return;
+            }
         }
         // header :84-106 and stream length words :110-112
         uint8_t *dst = a.out + ob;
         const uint32_t sdata[2] = {hdr + 4, hdr + 4 + 2 * P0m + 4};
-        if constexpr (TL == 0) {
+        if constexpr (TL == 0 && !DEFER) {
         for (uint32_t t = tid; t < hdr; t += TEAM) {
             const int f = t >> 2, sh = 8 * (t & 3);
             uint32_t v;
@@ -1560,6 +1577,57 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
             // took 3.
             const uint32_t cap6[2] = {1u + NB * 64u * Ls[0], 1u + NB * 64u * Ls[1]};
             bool fresh = true;
+            bool resolved = false;
+            // (DEFER) wave 0 completes the look-back at its first flush and publishes the offset
+            // in LDS; the other waves wait there for it.  Returns whether the blob fits.
+            auto resolve_lb = [&]() __attribute__((always_inline)) -> bool {
+                uint64_t b;
+                uint32_t ok;
+                if (wv == 0) {
+                    b = lookback_resolve(a.lookback, msg, Eblob, a.errflags);
+                    ok = b + Eblob <= a.out_cap ? 1u : 0u;
+                    uint8_t *hd = a.out + b;
+                    if (lane == 0) {
+                        a.out_off[msg] = b;
+                        if (msg == a.n_msgs - 1) a.out_off[a.n_msgs] = b + Eblob;
+                        if (a.status) a.status[msg] = ok ? ST_OK : ST_CAPACITY;
+                    }
+                    if (ok) {
+                        const uint32_t t = (uint32_t)lane;
+                        if (t < hdr) {
+                            const int f = t >> 2, sh = 8 * (t & 3);
+                            uint32_t v;
+                            if (f == 0) v = kMagicTDT;
+                            else if (f == 1) v = n32;
+                            else if (f == 2) v = ns;
+                            else if (f == 3 || f == 4) v = WS;
+                            else v = (mapbits >> (f - 5)) & 1u;
+                            hd[t] = (uint8_t)(v >> sh);
+                        } else if (t >= 48 && t < 56) {
+                            const int c = (t - 48) >> 2, sh = 8 * (t & 3);
+                            if ((uint32_t)c < ns) {
+                                const uint32_t len = 2 * (c ? P1 : P0);
+                                hd[sdata[c] - 4 + (t & 3)] = (uint8_t)(len >> sh);
+                            }
+                        }
+                    }
+                    if (lane == 0) {
+                        *reinterpret_cast<uint64_t *>(misc + M_BASE) = b;
+                        misc[M_BASE + 2] = ok;
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                        __hip_atomic_store(&wm[M_READY], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
+                } else {
+                    while (__hip_atomic_load(&wm[M_READY], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
+                        __builtin_amdgcn_s_sleep(2);
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                    b = *reinterpret_cast<const uint64_t *>(misc + M_BASE);
+                    ok = misc[M_BASE + 2];
+                }
+                b = rfl_u64(b);
+                dst = a.out + b;
+                return __builtin_amdgcn_readfirstlane(ok) != 0u;
+            };
             uint32_t rb = 0;  // the batch's first round
 #pragma unroll
             for (int r = 0; r < G; ++r) {
@@ -1575,6 +1643,12 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
                     const bool over = (hp[0] ? 1u : 0u) + s6[0] + 64u * Ls[0] > cap6[0] ||
                                       (ns2 && (hp[1] ? 1u : 0u) + s6[1] + 64u * Ls[1] > cap6[1]);
                     if (over || (uint32_t)(r + 1) == RW) {
+                        if constexpr (DEFER) {
+                            if (!resolved) {
+                                resolved = true;
+                                if (!resolve_lb()) return;  // TDT_E_CAPACITY: nothing is written
+                            }
+                        }
                         const uint32_t gb = gw0 + rb * 64u, ge = gw0 + (uint32_t)r * 64u + 64u;
                         flush6(gb <= ngroups - 1 && ngroups - 1 < ge);
                         fresh = true;

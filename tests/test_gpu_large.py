@@ -207,3 +207,50 @@ def test_large_decode_generic_shapes():
     b8 = orc.encode(x, cfg=orc.config(word_size=8), bandwidth=10.0, mapping=[1, 1, 1, 0, 0, 0, 0, 0])
     assert parse_blob(b8)[0][3] == 8
     decode_vs_oracle([b8, orc.encode(x, bandwidth=10.0)])
+
+
+def test_compacted_offsets_past_4gib():
+    """The compacted one-pass encode (decoupled look-back) over 6 GiB of C3-style messages:
+    blob offsets pass 2^31 and 2^32, so the 64-bit offsets must survive every wave-uniform
+    broadcast (a sign-extended low half faulted here).  Offsets equal the scan of the slotted
+    lengths, sampled blobs (first, around 2 / 4 GiB, last) equal the oracle's, and the round
+    trip is exact."""
+    codec = codec_for(4)
+    n, mb = 98304, 65536  # 6 GiB in, ~4.8 GiB of blobs
+    g = torch.Generator(device="cuda")
+    g.manual_seed(41)
+    x = torch.empty(n * mb // 4, dtype=torch.float32, device="cuda").normal_(0, 0.01, generator=g)
+    x.masked_fill_(torch.rand(x.numel(), device="cuda", generator=g) < 0.7, 0.0)
+    data = x.view(torch.uint8)
+    off = torch.arange(n + 1, dtype=torch.int64, device="cuda") * mb
+    out, eoff, st = codec.encode_batch(data, off)
+    torch.cuda.synchronize()
+    assert int(st.abs().sum()) == 0
+    eo = eoff.cpu().numpy()
+    assert eo[-1] > (1 << 32) and np.all(np.diff(eo) > 0)
+    # slotted lengths, scanned, give the same offsets
+    slots = codec.encode_slots(off)
+    buf = torch.empty(int(slots[-1].item()), dtype=torch.uint8, device="cuda")
+    lens = torch.empty(n, dtype=torch.int64, device="cuda")
+    sst = torch.empty(n, dtype=torch.int32, device="cuda")
+    from psyne_amd._lib import check
+    check(codec._lib.tdt_encode_batch_into(codec._h, data.data_ptr(), off.data_ptr(), n, buf.data_ptr(),
+                                           slots.data_ptr(), lens.data_ptr(), sst.data_ptr(),
+                                           torch.cuda.current_stream().cuda_stream))
+    torch.cuda.synchronize()
+    assert np.array_equal(np.diff(eo), lens.cpu().numpy())
+    del buf
+    orc = Oracle()
+    cfg = orc.config(sample_fraction=1.0)
+    picks = {0, n - 1}
+    for lim in (1 << 31, 1 << 32):
+        k = int(np.searchsorted(eo, lim))
+        picks.update({k - 1, k})
+    for i in sorted(picks):
+        m = data[i * mb:(i + 1) * mb].cpu().numpy()
+        assert out[eo[i]:eo[i + 1]].cpu().numpy().tobytes() == orc.encode(m, cfg=cfg, bandwidth=10.0), i
+    back, doff, dst = codec.decode_batch(out, eoff, out_capacity=n * mb,
+                                         out=torch.empty(n * mb, dtype=torch.uint8, device="cuda"))
+    torch.cuda.synchronize()
+    assert int(dst.abs().sum()) == 0 and torch.equal(back, data)
+    assert torch.equal(doff, off)
