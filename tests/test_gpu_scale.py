@@ -70,6 +70,21 @@ def test_c2_full_batch_bitexact():
     check_slotted(make_codec(), data, off)
 
 
+@pytest.mark.timeout(600)
+def test_c4_zipf_full_range_bitexact():
+    """C4's size distribution over its FULL range (bench.zipf_sizes: 64 B - 1 MiB, Zipf(1.5),
+    the C4 seed) on 500,000 messages (~3 GiB, every message class incl. the tiled > 256 KiB
+    path), gradient-like content generated on the device as bench.py --workload c4 does; every
+    blob of the slotted batch compared with the oracle, then decoded back."""
+    import bench
+    sizes = bench.zipf_sizes(500_000, 0x5EED0003)
+    assert sizes.max() > (256 << 10) and sizes.min() == 64  # the tiled and the UNCP classes occur
+    off = np.zeros(sizes.size + 1, np.int64)
+    off[1:] = np.cumsum(sizes)
+    data = bench.gen_gradient(torch, 1, int(off[-1]), 0x5EED0003, torch.device("cuda"))
+    check_slotted(make_codec(), data, torch.from_numpy(off).cuda(), chunk=65536)
+
+
 @pytest.mark.timeout(300)
 def test_100k_mixed_vs_oracle():
     """100,000 messages of 64 B - 8 KiB (UNCP below 1 KiB), half uniform bytes, half
