@@ -23,7 +23,7 @@ step rocprof
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
   python3 bench.py --steps 5 --warmup 2 --cpu-seconds 0 --compacted-steps 0 > "$OUT/prof_bench.log" 2>&1
 rc=$?; [ $rc -eq 0 ] || exit $rc
-python3 tools/prof_summary.py "$OUT/prof" "$OUT/kernel_stats.md" "rocprofv3 --kernel-trace --stats: bench.py --steps 5 --warmup 2 ($TAG)" > /dev/null
+python3 tools/prof_summary.py "$OUT/prof" "$OUT/kernel_stats.md" "rocprofv3 --kernel-trace --stats: bench.py --steps 5 --warmup 2 ($TAG)" --steady 5 > /dev/null
 step pmc
 bash tools/profile_pmc.sh "$OUT/pmc" || exit 1
 step c2_c4

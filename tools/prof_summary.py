@@ -1,8 +1,14 @@
 #!/usr/bin/env python3
 """Summarise rocprofv3 output (results .db or kernel_stats.csv) into a small markdown table.
 
-usage: python tools/prof_summary.py <rocprof output dir> <out.md> [title]
+usage: python tools/prof_summary.py <rocprof output dir> <out.md> [title] [--steady K]
+
+The table is rocprofv3's own --stats summary (every call, warm-up calls included).  With
+--steady K and a kernel trace present, a second table gives each psy:: kernel's average over
+its LAST K calls (the timed steps of the bench command, after its warm-up calls: the first call
+of a context runs without a plan history and on untouched output pages).
 """
+import collections
 import csv
 import glob
 import pathlib
@@ -26,9 +32,30 @@ def rows_from_csv(p):
     return out
 
 
+def steady_rows(trace, k):
+    per = collections.defaultdict(list)
+    with open(trace) as f:
+        for r in csv.DictReader(f):
+            if "psy::" not in r["Kernel_Name"]:
+                continue
+            per[r["Kernel_Name"]].append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
+    out = []
+    for name, v in per.items():
+        v.sort()
+        last = v[-k:]
+        out.append((name, len(last), sum(e - s for s, e in last) / len(last)))
+    return sorted(out, key=lambda x: -x[2] * x[1])
+
+
 def main():
-    d, out = pathlib.Path(sys.argv[1]), pathlib.Path(sys.argv[2])
-    title = sys.argv[3] if len(sys.argv) > 3 else str(d)
+    args = [a for a in sys.argv[1:]]
+    steady = 0
+    if "--steady" in args:
+        i = args.index("--steady")
+        steady = int(args[i + 1])
+        del args[i:i + 2]
+    d, out = pathlib.Path(args[0]), pathlib.Path(args[1])
+    title = args[2] if len(args) > 2 else str(d)
     dbs = glob.glob(str(d / "**" / "*.db"), recursive=True)
     csvs = glob.glob(str(d / "**" / "*kernel_stats.csv"), recursive=True)
     rows = rows_from_csv(csvs[0]) if csvs else rows_from_db(dbs[0])
@@ -36,6 +63,13 @@ def main():
     for name, calls, tot, avg, pct in rows[:12]:
         short = name if len(name) < 90 else name[:87] + "..."
         lines.append("| `%s` | %d | %.3f | %.1f | %.2f |" % (short, calls, tot / 1e6, avg / 1e3, pct))
+    traces = glob.glob(str(d / "**" / "*kernel_trace.csv"), recursive=True)
+    if steady and traces:
+        lines += ["", "Steady state: average over each psy:: kernel's last %d calls (the timed steps)." % steady, "",
+                  "| kernel | calls | avg us |", "|---|---|---|"]
+        for name, n, avg in steady_rows(traces[0], steady)[:12]:
+            short = name if len(name) < 90 else name[:87] + "..."
+            lines.append("| `%s` | %d | %.1f |" % (short, n, avg / 1e3))
     out.write_text("\n".join(lines) + "\n")
     print("\n".join(lines[:8]))
 
