@@ -234,6 +234,10 @@ int launch_encode_t(psy::EncodeArgs a, hipStream_t s) {
 // which takes any size), so repeated batches of one shape launch exactly what they need.
 // Calls are therefore asynchronous and capturable (hipGraphs).
 constexpr uint64_t kSmallMax = 4096;  // one-wave teams up to this size
+// 256-lane teams (4 waves, 8 resident rounds each: 32 KiB) above kSmallMax up to this size: a
+// message-sized 512-lane team would give each wave at most four rounds, and the per-wave fixed
+// work (entropy share, flush set-up, header) would weigh twice as much per byte
+constexpr uint64_t kMidMax = 32768;
 constexpr uint32_t kLmax = 1u << 16;   // large messages per batch (full budget)
 // tiles per batch at the full budget: 256 MiB of span histograms (WS KiB per 512 KiB span) —
 // 32 GiB of large messages at word size 4 (C4's 4 Mi-message Zipf batch holds 12 GiB of them);
@@ -252,7 +256,7 @@ uint32_t pow2_at_least(uint64_t x, uint32_t lo, uint32_t hi) {
 }
 
 int ensure_plan(PlanWS &w, uint32_t n, hipStream_t s) {
-    const size_t need = 256 + 8ull * n;
+    const size_t need = 256 + 12ull * n;  // counters | small | medium | mid-sized lists
     if (need > w.bytes) {
         if (int st = no_growth_in_capture(s)) return st;
         if (w.buf) HIPCHK(hipFree(w.buf));
@@ -355,6 +359,7 @@ int launch_slotted(tdt_ctx *c, PlanWS &pw, psy::EncodeArgs a, hipStream_t s) {
     if (!capturing) H.refresh();  // (event queries are not capturable)
     // classes an earlier plan found empty are off (their messages, if any, go medium)
     const bool small_on = !H.valid || H.v[10] > 0;  // (counter 5: small messages, listed or not)
+    const bool mid_on = !H.valid || H.v[14] > 0;    // (counter 7: mid-sized messages, listed or not)
     bool tiles_on = !H.valid || H.v[4] > 0;
     if (tiles_on && !capturing) {
         st = ensure_elarge(pw, WS, s);
@@ -363,7 +368,7 @@ int launch_slotted(tdt_ctx *c, PlanWS &pw, psy::EncodeArgs a, hipStream_t s) {
     tiles_on = tiles_on && pw.elarge;
     auto *cnt64 = reinterpret_cast<unsigned long long *>(pw.buf);
     auto *cnt = reinterpret_cast<uint32_t *>(pw.buf);  // cnt[2k]: the low word of counter k
-    uint32_t *slist = reinterpret_cast<uint32_t *>(pw.buf + 256), *mlist = slist + n;
+    uint32_t *slist = reinterpret_cast<uint32_t *>(pw.buf + 256), *mlist = slist + n, *qlist = mlist + n;
     const uint32_t lcap = tiles_on ? pw.e_lcap : 0u;
     const uint32_t tcap = tiles_on ? std::min(pw.e_tcap, std::max(c->tile_cap, psy::kSpanTiles)) : 0u;
     const uint32_t scap = tcap / psy::kSpanTiles;
@@ -374,15 +379,15 @@ int launch_slotted(tdt_ctx *c, PlanWS &pw, psy::EncodeArgs a, hipStream_t s) {
         reinterpret_cast<uint64_t *>(reinterpret_cast<uint8_t *>(trec) + sizeof(psy::TileRec) * pw.e_tcap);
     auto *shist = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(spans) + 8ull * (pw.e_tcap / psy::kSpanTiles));
     HIPCHK(hipMemsetAsync(cnt, 0, 64, s));
-    psy::PlanArgs p{a.in_off, n, cnt64, slist, mlist, tiles, spans, lmeta, lcap, tcap, kSmallMax, c->large_min,
-                    small_on ? 1u : 0u};
+    psy::PlanArgs p{a.in_off, n, cnt64, slist, mlist, qlist, tiles, spans, lmeta, lcap, tcap, kSmallMax, kMidMax,
+                    c->large_min, small_on ? 1u : 0u, mid_on ? 1u : 0u};
     const uint32_t per = psy::kPlanThreads * psy::kPlanPer;
     hipLaunchKernelGGL(psy::tdt_encode_plan_kernel, dim3((uint32_t)(((uint64_t)n + per - 1) / per)),
                        dim3(psy::kPlanThreads), 0, s, p);
     HIPCHK(hipGetLastError());
     if (!capturing && (st = record_counts(H, cnt, n, s))) return st;
     a.pcnt = cnt;
-    const uint32_t ovf512 = (uint32_t)c->cus * 3, ovf64 = (uint32_t)c->cus * 24;
+    const uint32_t ovf512 = (uint32_t)c->cus * 3, ovf256 = (uint32_t)c->cus * 6, ovf64 = (uint32_t)c->cus * 24;
     // main launch over [0, g) + overflow launch over [g, count) of one class
     auto both = [&](uint32_t g, uint32_t bound, uint32_t ovf, auto &&main, auto &&over) {
         if (g) main(0u, g);
@@ -456,6 +461,25 @@ int launch_slotted(tdt_ctx *c, PlanWS &pw, psy::EncodeArgs a, hipStream_t s) {
                  a.list_base = b;
                  hipLaunchKernelGGL((psy::tdt_encode_kernel<WS, 64, 4, MODE_ENCODE, 0, 0, 1>), dim3(g), dim3(64), 0,
                                     ss, a);
+             });
+    }
+    // mid-sized messages (256-lane teams) on the small list's stream
+    if (mid_on) {
+        const hipStream_t qs = forked && !c->small_main ? pw.side : s;
+        a.list = qlist;
+        a.list_count = cnt + 12;
+        both(guess(H, 12, n, n), n, ovf256,
+             [&](uint32_t b, uint32_t g) {
+                 launch_list(g, 256, [&](uint32_t b2, uint32_t g2) {
+                     a.list_base = b + b2;
+                     hipLaunchKernelGGL((psy::tdt_encode_kernel<WS, 256, 8, MODE_ENCODE, 0, 0, 0>), dim3(g2),
+                                        dim3(256), 0, qs, a);
+                 });
+             },
+             [&](uint32_t b, uint32_t g) {
+                 a.list_base = b;
+                 hipLaunchKernelGGL((psy::tdt_encode_kernel<WS, 256, 8, MODE_ENCODE, 0, 0, 1>), dim3(g), dim3(256), 0,
+                                    qs, a);
              });
     }
     if (forked) return join_side(pw, s);

@@ -132,7 +132,9 @@ struct EncLayout {
     static constexpr int bin(int v, int k) { return (v - 1) * HC + k; }  // v >= 1
     static constexpr int HIST = WS * PS * 4;
     static constexpr int HISTA = HIST;
-    static constexpr int TB = (TEAM >= 256) ? (WS < 4 ? WS : 4) : 1;
+    // positions per batch of the exact (tie) path: 4 for message-sized teams; one for the
+    // 256-lane team, whose LDS footprint (staging of 4 waves) sets its occupancy
+    static constexpr int TB = (TEAM >= 512) ? (WS < 4 ? WS : 4) : 1;
     // one stream's pairs of one wave-round: alignment pad + 1024 pairs + one garbage pair
     static constexpr int WREGION = 16 + 2 * 64 * 16 + 16;
     // per wave: v4 emit — both streams' pair windows + a junk pair; v5 emit — 64 junk dwords,
@@ -290,7 +292,7 @@ __device__ __forceinline__ uint32_t spread2(uint32_t e) {
 #ifndef PSY_ENC_WPE
 #define PSY_ENC_WPE 6
 #endif
-#define PSY_ENC_WAVES(TEAM) ((TEAM) >= 512 ? PSY_ENC_WPE : 7)
+#define PSY_ENC_WAVES(TEAM) ((TEAM) >= 256 ? PSY_ENC_WPE : 7)
 
 // One message — or, TL > 0, part of a large message: TL 1 the histogram of one span of
 // kSpanTiles tiles (UNCP messages: the span's copy), 4 the mapping from the message's span
@@ -1768,14 +1770,16 @@ struct PlanArgs {
     const uint64_t *in_off;
     uint32_t n_msgs;
     // [0] small (listed), [1] medium, [2] large entries, [3] tiles, [4] spans claimed, [5] small
-    // messages (listed or not: the host's count history switches the small class back on)
+    // messages (listed or not: the host's count history switches the small class back on), [6]
+    // mid-sized (listed), [7] mid-sized messages (listed or not)
     unsigned long long *cnt;
-    uint32_t *slist, *mlist;
+    uint32_t *slist, *mlist, *qlist;
     uint64_t *tiles, *spans;
     LMeta *lmeta;
     uint32_t lmax, tile_cap;  // span_cap = tile_cap / kSpanTiles (0, 0: no tiled path)
-    uint64_t small_max, large_min;
+    uint64_t small_max, mid_max, large_min;
     uint32_t small_on;  // 0: small messages join the medium list
+    uint32_t mid_on;    // 0: mid-sized messages join the medium list
 };
 
 constexpr uint32_t kPlanThreads = 1024, kPlanPer = 2;  // messages per plan workgroup: 2048
@@ -1797,6 +1801,7 @@ __global__ __launch_bounds__(kPlanThreads) void tdt_encode_plan_kernel(PlanArgs 
     wg_claim<kPlanPer>(T, t0, p.cnt + 3, lds);
     wg_claim<kPlanPer>(S, s0, p.cnt + 4, lds);
     uint64_t sm[kPlanPer], md[kPlanPer], ps[kPlanPer], pm[kPlanPer], sc[kPlanPer], pc[kPlanPer];
+    uint64_t qm[kPlanPer], pq[kPlanPer], qc[kPlanPer], pqc[kPlanPer];
 #pragma unroll
     for (int k = 0; k < (int)kPlanPer; ++k) {
         const uint32_t i = (blockIdx.x * kPlanPer + k) * kPlanThreads + threadIdx.x;
@@ -1821,18 +1826,24 @@ __global__ __launch_bounds__(kPlanThreads) void tdt_encode_plan_kernel(PlanArgs 
         }
         const bool valid = i < p.n_msgs;
         const bool small = valid && !isl[k] && n[k] <= p.small_max;
+        const bool mid = valid && !isl[k] && !small && n[k] <= p.mid_max;
         sc[k] = small ? 1u : 0u;
         sm[k] = small && p.small_on ? 1u : 0u;
-        md[k] = valid && !large && !sm[k] ? 1u : 0u;
+        qc[k] = mid ? 1u : 0u;
+        qm[k] = mid && p.mid_on ? 1u : 0u;
+        md[k] = valid && !large && !sm[k] && !qm[k] ? 1u : 0u;
     }
     wg_claim<kPlanPer>(sm, ps, p.cnt + 0, lds);
     wg_claim<kPlanPer>(md, pm, p.cnt + 1, lds);
     wg_claim<kPlanPer>(sc, pc, p.cnt + 5, lds);
+    wg_claim<kPlanPer>(qm, pq, p.cnt + 6, lds);
+    wg_claim<kPlanPer>(qc, pqc, p.cnt + 7, lds);
 #pragma unroll
     for (int k = 0; k < (int)kPlanPer; ++k) {
         const uint32_t i = (blockIdx.x * kPlanPer + k) * kPlanThreads + threadIdx.x;
         if (sm[k]) p.slist[ps[k]] = i;
         if (md[k]) p.mlist[pm[k]] = i;
+        if (qm[k]) p.qlist[pq[k]] = i;
     }
 }
 
@@ -1933,6 +1944,7 @@ __global__ __launch_bounds__(64) void tdt_encode_lscan_kernel(EncodeArgs a, cons
     X(WS, 512, 8, MODE_ENCODE, 0, 3, 0) X(WS, 512, 8, MODE_ENCODE, 0, 4, 0) X(WS, 64, 4, MODE_ENCODE, 0, 0, 0)  \
     X(WS, 512, 8, MODE_ENCODE, 0, 0, 1) X(WS, 512, 8, MODE_ENCODE, 0, 1, 1) X(WS, 512, 8, MODE_ENCODE, 0, 2, 1) \
     X(WS, 512, 8, MODE_ENCODE, 0, 3, 1) X(WS, 512, 8, MODE_ENCODE, 0, 4, 1) X(WS, 64, 4, MODE_ENCODE, 0, 0, 1)  \
+    X(WS, 256, 8, MODE_ENCODE, 0, 0, 0) X(WS, 256, 8, MODE_ENCODE, 0, 0, 1)                                     \
     X(WS, 64, 4, MODE_ENCODE, 1, 0, 0) X(WS, 512, 8, MODE_ENCODE, 1, 0, 0) X(WS, 64, 4, MODE_MAPPED, 1, 0, 0)   \
     X(WS, 512, 8, MODE_MAPPED, 1, 0, 0) X(WS, 64, 4, MODE_ANALYZE, 1, 0, 0) X(WS, 512, 8, MODE_ANALYZE, 1, 0, 0)
 

@@ -86,6 +86,27 @@ def test_c4_zipf_full_range_bitexact():
 
 
 @pytest.mark.timeout(300)
+def test_mid_class_slotted():
+    """The 256-lane class (4 KiB < n <= 32 KiB) beside its neighbours: 3,000 messages of every
+    size around the class bounds and inside it (multiples of 4 and not, so most start
+    unaligned: the streaming body), gradient-like and uniform, every slotted blob compared with
+    the oracle, then decoded back."""
+    rng = np.random.default_rng(61)
+    edges = [4092, 4096, 4100, 4104, 8192, 16380, 16384, 16388, 32764, 32768, 32772, 32776, 65536]
+    sizes = np.concatenate([np.array(edges * 40, np.int64), rng.integers(4097, 32769, 2480)])
+    rng.shuffle(sizes)
+    off = np.zeros(sizes.size + 1, np.int64)
+    off[1:] = np.cumsum(sizes)
+    buf = rng.integers(0, 256, int(off[-1]), dtype=np.uint8)
+    for i in range(0, sizes.size, 2):
+        k = int(sizes[i]) // 4
+        x = rng.normal(0, 0.01, k).astype(np.float32)
+        x[rng.random(k) < 0.7] = 0
+        buf[off[i]:off[i] + 4 * k] = x.view(np.uint8)
+    check_slotted(make_codec(), torch.from_numpy(buf).cuda(), torch.from_numpy(off).cuda())
+
+
+@pytest.mark.timeout(300)
 def test_100k_mixed_vs_oracle():
     """100,000 messages of 64 B - 8 KiB (UNCP below 1 KiB), half uniform bytes, half
     gradient-like float32, every blob compared with the oracle."""
