@@ -394,12 +394,17 @@ int launch_slotted(tdt_ctx *c, PlanWS &pw, psy::EncodeArgs a, hipStream_t s) {
         if (g < bound) over(g, std::min(ovf, bound - g));
     };
     bool forked = false;
-    hipStream_t ts = s;  // the tile pipeline's (and the small list's) stream
-    if (tiles_on) {
+    hipStream_t ts = s;  // the tile pipeline's (and the small / mid-sized lists') stream
+    // the side stream carries the tile pipeline and the small / mid-sized lists beside the medium
+    // list (queued behind it on one stream they would run alone in its tail)
+    const bool medium_on = !H.valid || H.v[2] > 0;
+    if (tiles_on || ((small_on || mid_on) && medium_on && !c->small_main)) {
         const int fr = c->no_side ? -1 : fork_side(pw, s);
         if (fr > 0) return fr;
         forked = fr == TDT_OK;
         if (forked) ts = pw.side;
+    }
+    if (tiles_on) {
         a.tiles = tiles;
         a.spans = spans;
         a.lmeta = lmeta;
@@ -697,11 +702,16 @@ int launch_decode_slotted(tdt_ctx *c, PlanWS &pw, psy::DecodeArgs a, hipStream_t
     };
     bool forked = false;
     hipStream_t ts = s;
-    if (large_on) {
+    // the side stream carries the large-blob pipeline and the small-blob list beside the main
+    // list (the small list queued behind the main list ran alone in its tail: C4 1.6 ms)
+    const bool main_on = !H.valid || H.v[0] > 0;
+    if (large_on || (small_on && main_on && !c->small_main)) {
         const int fr = c->no_side ? -1 : fork_side(pw, s);
         if (fr > 0) return fr;
         forked = fr == TDT_OK;
         if (forked) ts = pw.side;
+    }
+    if (large_on) {
         const uint32_t gl = std::max(1u, std::min(lcap, 1024u));
         hipLaunchKernelGGL(psy::tdt_decode_lprep_kernel, dim3(gl), dim3(256), 0, ts, a);
         hipLaunchKernelGGL(psy::tdt_decode_lblock_kernel, dim3(std::max(1u, std::min((bcap + 3) / 4, ovf / 4))),
