@@ -612,8 +612,8 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
             constexpr int BPT = TP >= 256 ? 1 : 256 / TP;
             const int pb = tid / TP, pj = tid % TP;
             // c·log2 c per bin in float (an empty bin: 0·log2 1 = 0), summed in float over groups of
-            // at most 16 bins and in double across groups: K <= 16 roundings of 2^-24 relative each
-            // add at most 16·2^-24·log2 N <= 1.4e-5 bits to the hardware log's 2^-18
+            // at most 16 bins and in double across groups: <= 17 roundings of 2^-24 relative each
+            // add at most 17·2^-24·log2 N < 3.3e-5 bits to the hardware log's 2^-18
             double acc = 0.0;
 #pragma unroll
             for (int k0 = 0; k0 < BPT; k0 += 16) {
