@@ -76,7 +76,7 @@ struct CountHist {
     uint32_t *pin = nullptr;  // pinned: the plan's 8 u64 counters
     hipEvent_t ev = nullptr;
     bool pending = false, valid = false;
-    uint32_t v[16] = {};
+    uint32_t v[32] = {};
     uint32_t n = 0, n_pending = 0;  // messages in the snapshot's batch
     // fold the newest completed snapshot in (never waits)
     void refresh() {
@@ -234,6 +234,9 @@ int launch_encode_t(psy::EncodeArgs a, hipStream_t s) {
 // which takes any size), so repeated batches of one shape launch exactly what they need.
 // Calls are therefore asynchronous and capturable (hipGraphs).
 constexpr uint64_t kSmallMax = 4096;  // one-wave teams up to this size
+// medium messages above this (the streaming body: more than 8 resident rounds per wave) are
+// dispatched first
+constexpr uint64_t kBigMin = 65536;
 // 256-lane teams (4 waves, 8 resident rounds each: 32 KiB) above kSmallMax up to this size: a
 // message-sized 512-lane team would give each wave at most four rounds, and the per-wave fixed
 // work (entropy share, flush set-up, header) would weigh twice as much per byte
@@ -256,7 +259,7 @@ uint32_t pow2_at_least(uint64_t x, uint32_t lo, uint32_t hi) {
 }
 
 int ensure_plan(PlanWS &w, uint32_t n, hipStream_t s) {
-    const size_t need = 256 + 12ull * n;  // counters | small | medium | mid-sized lists
+    const size_t need = 256 + 16ull * n;  // counters | small | medium | mid-sized | big lists
     if (need > w.bytes) {
         if (int st = no_growth_in_capture(s)) return st;
         if (w.buf) HIPCHK(hipFree(w.buf));
@@ -271,10 +274,10 @@ int ensure_plan(PlanWS &w, uint32_t n, hipStream_t s) {
 // The plan counters of this call → pinned snapshot (not under stream capture).
 int record_counts(CountHist &h, const void *dcnt, uint32_t n_msgs, hipStream_t s) {
     if (!h.pin) {
-        HIPCHK(hipHostMalloc(&h.pin, 64, hipHostMallocDefault));
+        HIPCHK(hipHostMalloc(&h.pin, 128, hipHostMallocDefault));
         HIPCHK(hipEventCreateWithFlags(&h.ev, hipEventDisableTiming));
     }
-    HIPCHK(hipMemcpyAsync(h.pin, dcnt, 64, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(h.pin, dcnt, 128, hipMemcpyDeviceToHost, s));
     HIPCHK(hipEventRecord(h.ev, s));
     h.n_pending = n_msgs;
     h.pending = true;
@@ -368,7 +371,8 @@ int launch_slotted(tdt_ctx *c, PlanWS &pw, psy::EncodeArgs a, hipStream_t s) {
     tiles_on = tiles_on && pw.elarge;
     auto *cnt64 = reinterpret_cast<unsigned long long *>(pw.buf);
     auto *cnt = reinterpret_cast<uint32_t *>(pw.buf);  // cnt[2k]: the low word of counter k
-    uint32_t *slist = reinterpret_cast<uint32_t *>(pw.buf + 256), *mlist = slist + n, *qlist = mlist + n;
+    uint32_t *slist = reinterpret_cast<uint32_t *>(pw.buf + 256), *mlist = slist + n, *qlist = mlist + n,
+             *blist = qlist + n;
     const uint32_t lcap = tiles_on ? pw.e_lcap : 0u;
     const uint32_t tcap = tiles_on ? std::min(pw.e_tcap, std::max(c->tile_cap, psy::kSpanTiles)) : 0u;
     const uint32_t scap = tcap / psy::kSpanTiles;
@@ -378,9 +382,9 @@ int launch_slotted(tdt_ctx *c, PlanWS &pw, psy::EncodeArgs a, hipStream_t s) {
     auto *spans =
         reinterpret_cast<uint64_t *>(reinterpret_cast<uint8_t *>(trec) + sizeof(psy::TileRec) * pw.e_tcap);
     auto *shist = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(spans) + 8ull * (pw.e_tcap / psy::kSpanTiles));
-    HIPCHK(hipMemsetAsync(cnt, 0, 64, s));
-    psy::PlanArgs p{a.in_off, n, cnt64, slist, mlist, qlist, tiles, spans, lmeta, lcap, tcap, kSmallMax, kMidMax,
-                    c->large_min, small_on ? 1u : 0u, mid_on ? 1u : 0u};
+    HIPCHK(hipMemsetAsync(cnt, 0, 128, s));
+    psy::PlanArgs p{a.in_off,  n,    cnt64,     slist,   mlist,   qlist, blist, tiles, spans, lmeta, lcap, tcap,
+                    kSmallMax, kMidMax, kBigMin, c->large_min, small_on ? 1u : 0u, mid_on ? 1u : 0u};
     const uint32_t per = psy::kPlanThreads * psy::kPlanPer;
     hipLaunchKernelGGL(psy::tdt_encode_plan_kernel, dim3((uint32_t)(((uint64_t)n + per - 1) / per)),
                        dim3(psy::kPlanThreads), 0, s, p);
@@ -397,7 +401,7 @@ int launch_slotted(tdt_ctx *c, PlanWS &pw, psy::EncodeArgs a, hipStream_t s) {
     hipStream_t ts = s;  // the tile pipeline's (and the small / mid-sized lists') stream
     // the side stream carries the tile pipeline and the small / mid-sized lists beside the medium
     // list (queued behind it on one stream they would run alone in its tail)
-    const bool medium_on = !H.valid || H.v[2] > 0;
+    const bool medium_on = !H.valid || H.v[2] + H.v[16] > 0;  // (counters 1 and 8)
     if (tiles_on || ((small_on || mid_on) && medium_on && !c->small_main)) {
         const int fr = c->no_side ? -1 : fork_side(pw, s);
         if (fr > 0) return fr;
@@ -432,10 +436,13 @@ int launch_slotted(tdt_ctx *c, PlanWS &pw, psy::EncodeArgs a, hipStream_t s) {
         PSY_TILE_STEP(3, 6, tcap);  // emit
 #undef PSY_TILE_STEP
     }
-    // medium messages: one workgroup per list entry
+    // medium messages: one workgroup per list entry (the streaming-size ones first)
     a.list = mlist;
     a.list_count = cnt + 2;
-    both(guess(H, 2, n, n), n, ovf512,
+    a.list2 = blist;
+    a.list2_count = cnt + 16;
+    const uint32_t gmed = H.valid ? std::min<uint32_t>(n, guess(H, 2, n, n) + guess(H, 16, n, n)) : n;
+    both(gmed, n, ovf512,
          [&](uint32_t b, uint32_t g) {
              launch_list(g, 512, [&](uint32_t b2, uint32_t g2) {
                  a.list_base = b + b2;
@@ -448,6 +455,7 @@ int launch_slotted(tdt_ctx *c, PlanWS &pw, psy::EncodeArgs a, hipStream_t s) {
              hipLaunchKernelGGL((psy::tdt_encode_kernel<WS, 512, 8, MODE_ENCODE, 0, 0, 1>), dim3(g), dim3(512), 0, s,
                                 a);
          });
+    a.list2 = nullptr;
     // small messages behind the tile pipeline on the side stream (the two streams' loads balance
     // better: C4's tile pipeline is shorter than its medium list)
     if (small_on) {
@@ -624,6 +632,7 @@ int encode_common(tdt_ctx *c, int mode, const uint8_t *d_in, const uint64_t *d_i
 constexpr uint32_t kDLmax = 1u << 16, kDBcap = 1u << 23, kDTcap = 1u << 20;  // full budgets
 constexpr uint32_t kDL0 = 1024, kDB0 = 1u << 16, kDT0 = 8192;                 // starting budgets
 constexpr uint64_t kDSmallMax = 1024;  // decoded sizes up to one window of one round
+constexpr uint64_t kDBigMin = 128 * 1024;  // one-wave blobs above this are dispatched first
 size_t dlarge_bytes(uint32_t lcap, uint32_t bcap, uint32_t tcap) {
     return (size_t)lcap * sizeof(psy::DMeta) + 8ull * bcap + 4ull * tcap + 8ull * tcap;
 }
@@ -667,15 +676,15 @@ int launch_decode_slotted(tdt_ctx *c, PlanWS &pw, psy::DecodeArgs a, hipStream_t
     auto *cnt = reinterpret_cast<unsigned long long *>(pw.buf);
     auto *cnt32 = reinterpret_cast<uint32_t *>(pw.buf);
     auto *list = reinterpret_cast<uint32_t *>(pw.buf + 256);
-    uint32_t *slist = list + n;
+    uint32_t *slist = list + n, *blist = slist + n;
     const uint32_t lcap = large_on ? pw.d_lcap : 0u, bcap = large_on ? pw.d_bcap : 0u,
                    tcap = large_on ? pw.d_tcap : 0u;
     auto *dmeta = reinterpret_cast<psy::DMeta *>(pw.dlarge);
     auto *bent = reinterpret_cast<uint32_t *>(pw.dlarge + (size_t)pw.d_lcap * sizeof(psy::DMeta));
     uint32_t *bsum = bent + pw.d_bcap, *tent = bsum + pw.d_bcap, *tblk = tent + pw.d_tcap;
-    HIPCHK(hipMemsetAsync(cnt, 0, 64, s));
-    psy::DPlanArgs p{a.in, a.in_off, a.in_len, n, cnt, list, slist, kDSmallMax, dmeta, bent, tent,
-                     lcap, bcap, tcap, c->large_min, small_on ? 1u : 0u};
+    HIPCHK(hipMemsetAsync(cnt, 0, 128, s));
+    psy::DPlanArgs p{a.in, a.in_off, a.in_len, n, cnt, list, slist, kDSmallMax, blist, kDBigMin, dmeta, bent,
+                     tent, lcap, bcap, tcap, c->large_min, small_on ? 1u : 0u};
     hipLaunchKernelGGL(psy::tdt_decode_plan_kernel, dim3((uint32_t)(((uint64_t)n + 4095) / 4096)), dim3(1024), 0, s, p);
     HIPCHK(hipGetLastError());
     if (!capturing && (st = record_counts(H, cnt, n, s))) return st;
@@ -704,7 +713,7 @@ int launch_decode_slotted(tdt_ctx *c, PlanWS &pw, psy::DecodeArgs a, hipStream_t
     hipStream_t ts = s;
     // the side stream carries the large-blob pipeline and the small-blob list beside the main
     // list (the small list queued behind the main list ran alone in its tail: C4 1.6 ms)
-    const bool main_on = !H.valid || H.v[0] > 0;
+    const bool main_on = !H.valid || H.v[0] + H.v[12] > 0;  // (counters 0 and 6)
     if (large_on || (small_on && main_on && !c->small_main)) {
         const int fr = c->no_side ? -1 : fork_side(pw, s);
         if (fr > 0) return fr;
@@ -729,7 +738,11 @@ int launch_decode_slotted(tdt_ctx *c, PlanWS &pw, psy::DecodeArgs a, hipStream_t
     }
     a.list = list;
     a.list_count = cnt32;
-    lists(guess(H, 0, n, n), s, psy::tdt_decode_kernel<0, psy::kDecWR, 0>, psy::tdt_decode_kernel<0, psy::kDecWR, 1>);
+    a.blist = blist;
+    a.blist_count = cnt32 + 12;
+    const uint32_t gmain = H.valid ? std::min<uint32_t>(n, guess(H, 0, n, n) + guess(H, 12, n, n)) : n;
+    lists(gmain, s, psy::tdt_decode_kernel<0, psy::kDecWR, 0>, psy::tdt_decode_kernel<0, psy::kDecWR, 1>);
+    a.blist = nullptr;
     // small blobs: one-round windows (a third less LDS per wave: more blobs in flight per CU)
     if (small_on) {
         a.list = slist;

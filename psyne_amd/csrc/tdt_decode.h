@@ -48,6 +48,10 @@ struct DecodeArgs {
     const uint32_t *list;
     const uint32_t *list_count;  // the list's length (device memory: the plan's counter)
     uint32_t list_base;
+    // (main list only) blobs decoding to more than big_min bytes, dispatched before `list`: a
+    // one-wave blob of up to 1 MiB started late would run alone in the kernel's tail
+    const uint32_t *blist;
+    const uint32_t *blist_count;
     // the plan's counters (u32 view: [2] large blobs, [4] tiles, [6] blocks claimed) and the
     // budgets it ran with
     const uint32_t *pcnt;
@@ -1089,11 +1093,14 @@ struct DPlanArgs {
     const uint64_t *in_len;
     uint32_t n_msgs;
     // [0] one-wave blobs, [1] large blobs, [2] tiles, [3] block slots, [4] small blobs (listed),
-    // [5] small blobs (listed or not: the host's count history switches the small list back on)
+    // [5] small blobs (listed or not: the host's count history switches the small list back on),
+    // [6] big one-wave blobs (their own list, dispatched first)
     unsigned long long *cnt;
     uint32_t *list;
     uint32_t *slist;          // blobs decoding to <= small_max bytes (one-round windows: less LDS per wave)
     uint64_t small_max;
+    uint32_t *blist;          // one-wave blobs decoding to > big_min bytes (dispatched first)
+    uint64_t big_min;
     DMeta *dmeta;
     uint32_t *bent, *tent;
     uint32_t lmax, bcap, tcap;  // (0, 0, 0: no tiled path)
@@ -1111,7 +1118,7 @@ __global__ __launch_bounds__(1024) void tdt_decode_plan_kernel(DPlanArgs p) {
         const uint64_t share = (last - p.in_off[0]) / 4096;
         thr = share > thr ? share : thr;
     }
-    uint64_t isl[4], nt[4], nb[4], j[4], t0[4], b0[4], one[4], pos[4], sm[4], spos[4], sc[4], scp[4];
+    uint64_t isl[4], nt[4], nb[4], j[4], t0[4], b0[4], one[4], pos[4], sm[4], spos[4], sc[4], scp[4], bg[4], bpos[4];
     uint64_t osz_k[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -1166,15 +1173,19 @@ __global__ __launch_bounds__(1024) void tdt_decode_plan_kernel(DPlanArgs p) {
         const bool small = any && !isl[k] && p.small_max && osz_k[k] <= p.small_max;
         sc[k] = small ? 1u : 0u;
         sm[k] = small && p.small_on ? 1u : 0u;
-        one[k] = (any && !sm[k]) ? 1u : 0u;
+        const bool big = any && !sm[k] && p.blist && osz_k[k] > p.big_min;
+        bg[k] = big ? 1u : 0u;
+        one[k] = (any && !sm[k] && !big) ? 1u : 0u;
     }
     wg_claim<4>(one, pos, p.cnt, lds);
     wg_claim<4>(sm, spos, p.cnt + 4, lds);
     wg_claim<4>(sc, scp, p.cnt + 5, lds);
+    wg_claim<4>(bg, bpos, p.cnt + 6, lds);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         if (one[k]) p.list[pos[k]] = (blockIdx.x * 4 + k) * 1024 + threadIdx.x;
         if (sm[k]) p.slist[spos[k]] = (blockIdx.x * 4 + k) * 1024 + threadIdx.x;
+        if (bg[k]) p.blist[bpos[k]] = (blockIdx.x * 4 + k) * 1024 + threadIdx.x;
     }
 }
 
@@ -1371,17 +1382,19 @@ __global__ __launch_bounds__(64, LB ? 6 : 8) void tdt_decode_kernel(DecodeArgs a
         if (lane_id() == 0) t = atomicAdd(a.ticket, 1u);
         decode_one<LB, WR>(a, smem, __builtin_amdgcn_readfirstlane(t));
     } else {
-        // (slotted launches always pass the plan's list)
-        const uint32_t cnt = __builtin_amdgcn_readfirstlane(*a.list_count);
+        // (slotted launches always pass the plan's list; the main list's big blobs come first)
+        const uint32_t nb = a.blist ? __builtin_amdgcn_readfirstlane(*a.blist_count) : 0u;
+        const uint32_t cnt = nb + __builtin_amdgcn_readfirstlane(*a.list_count);
         const uint32_t i0 = a.list_base + blockIdx.x;
+        auto entry = [&](uint32_t i) -> uint32_t { return i < nb ? a.blist[i] : a.list[i - nb]; };
         if constexpr (PS) {
             for (uint32_t i = i0; i < cnt; i += gridDim.x) {
                 if (i != i0) team_sync<1>();
-                decode_one<LB, WR>(a, smem, a.list[i]);
+                decode_one<LB, WR>(a, smem, entry(i));
             }
         } else {
             if (i0 >= cnt) return;
-            decode_one<LB, WR>(a, smem, a.list[i0]);
+            decode_one<LB, WR>(a, smem, entry(i0));
         }
     }
 }

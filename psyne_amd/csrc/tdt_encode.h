@@ -106,6 +106,10 @@ struct EncodeArgs {
     const uint32_t *list;
     const uint32_t *list_count;  // the list's length (device memory: the plan's counter)
     uint32_t list_base;  // first list / tile entry of this launch (grids of < 2^32 threads)
+    // (medium list only) the streaming-size messages, dispatched before `list`: a 256 KiB team
+    // started late would run alone in the kernel's tail
+    const uint32_t *list2;
+    const uint32_t *list2_count;
     // tiled large messages: tile / span entries (L index | tile << 32); the plan's counters
     // (u32 view: [4] large messages, [6] tiles, [8] spans claimed) and the budgets it ran with
     const uint64_t *tiles;
@@ -1720,7 +1724,7 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
 template <int TL>
 __device__ __forceinline__ uint32_t entry_count(const EncodeArgs &a) {
     uint32_t c;
-    if constexpr (TL == 0) c = *a.list_count;
+    if constexpr (TL == 0) c = *a.list_count + (a.list2 ? *a.list2_count : 0u);
     else if constexpr (TL == 4) c = umin(a.pcnt[4], a.lcap);
     else if constexpr (TL == 1) c = umin(a.pcnt[8], a.tcap / kSpanTiles);
     else c = umin(a.pcnt[6], a.tcap);
@@ -1740,9 +1744,10 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
         return;
     } else {
         // (slotted launches always pass a class list)
+        const uint32_t n2 = TL == 0 && a.list2 ? __builtin_amdgcn_readfirstlane(*a.list2_count) : 0u;
         auto one = [&](uint32_t i) __attribute__((always_inline)) {
             if constexpr (TL == 0) {
-                encode_one<WS, TEAM, G, MODE, LB, 0>(a, smem, a.list[i], 0, 0);
+                encode_one<WS, TEAM, G, MODE, LB, 0>(a, smem, i < n2 ? a.list2[i] : a.list[i - n2], 0, 0);
             } else if constexpr (TL == 4) {
                 const uint32_t msg = a.lmeta[i].msg;  // one large message per workgroup
                 if (msg != kNone) encode_one<WS, TEAM, G, MODE, LB, TL>(a, smem, msg, i, 0);
@@ -1779,13 +1784,14 @@ struct PlanArgs {
     uint32_t n_msgs;
     // [0] small (listed), [1] medium, [2] large entries, [3] tiles, [4] spans claimed, [5] small
     // messages (listed or not: the host's count history switches the small class back on), [6]
-    // mid-sized (listed), [7] mid-sized messages (listed or not)
+    // mid-sized (listed), [7] mid-sized messages (listed or not), [8] medium messages over big_min
+    // (their own list, dispatched first)
     unsigned long long *cnt;
-    uint32_t *slist, *mlist, *qlist;
+    uint32_t *slist, *mlist, *qlist, *blist;
     uint64_t *tiles, *spans;
     LMeta *lmeta;
     uint32_t lmax, tile_cap;  // span_cap = tile_cap / kSpanTiles (0, 0: no tiled path)
-    uint64_t small_max, mid_max, large_min;
+    uint64_t small_max, mid_max, big_min, large_min;
     uint32_t small_on;  // 0: small messages join the medium list
     uint32_t mid_on;    // 0: mid-sized messages join the medium list
 };
@@ -1809,7 +1815,7 @@ __global__ __launch_bounds__(kPlanThreads) void tdt_encode_plan_kernel(PlanArgs 
     wg_claim<kPlanPer>(T, t0, p.cnt + 3, lds);
     wg_claim<kPlanPer>(S, s0, p.cnt + 4, lds);
     uint64_t sm[kPlanPer], md[kPlanPer], ps[kPlanPer], pm[kPlanPer], sc[kPlanPer], pc[kPlanPer];
-    uint64_t qm[kPlanPer], pq[kPlanPer], qc[kPlanPer], pqc[kPlanPer];
+    uint64_t qm[kPlanPer], pq[kPlanPer], qc[kPlanPer], pqc[kPlanPer], bm[kPlanPer], pb[kPlanPer];
 #pragma unroll
     for (int k = 0; k < (int)kPlanPer; ++k) {
         const uint32_t i = (blockIdx.x * kPlanPer + k) * kPlanThreads + threadIdx.x;
@@ -1839,19 +1845,23 @@ __global__ __launch_bounds__(kPlanThreads) void tdt_encode_plan_kernel(PlanArgs 
         sm[k] = small && p.small_on ? 1u : 0u;
         qc[k] = mid ? 1u : 0u;
         qm[k] = mid && p.mid_on ? 1u : 0u;
-        md[k] = valid && !large && !sm[k] && !qm[k] ? 1u : 0u;
+        const bool medium = valid && !large && !sm[k] && !qm[k];
+        bm[k] = medium && p.blist && n[k] > p.big_min ? 1u : 0u;
+        md[k] = medium && !bm[k] ? 1u : 0u;
     }
     wg_claim<kPlanPer>(sm, ps, p.cnt + 0, lds);
     wg_claim<kPlanPer>(md, pm, p.cnt + 1, lds);
     wg_claim<kPlanPer>(sc, pc, p.cnt + 5, lds);
     wg_claim<kPlanPer>(qm, pq, p.cnt + 6, lds);
     wg_claim<kPlanPer>(qc, pqc, p.cnt + 7, lds);
+    wg_claim<kPlanPer>(bm, pb, p.cnt + 8, lds);
 #pragma unroll
     for (int k = 0; k < (int)kPlanPer; ++k) {
         const uint32_t i = (blockIdx.x * kPlanPer + k) * kPlanThreads + threadIdx.x;
         if (sm[k]) p.slist[ps[k]] = i;
         if (md[k]) p.mlist[pm[k]] = i;
         if (qm[k]) p.qlist[pq[k]] = i;
+        if (bm[k]) p.blist[pb[k]] = i;
     }
 }
 
