@@ -1449,6 +1449,7 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
         // 256) and NB rounds (3 for message-sized teams) share one flush: the per-round flush bookkeeping (pointers, the
         // last-entry read, the pending entry, loop set-up) is paid once per pair of rounds.
         constexpr bool E6 = RES && WS <= 4;
+        constexpr bool E6S = WS <= 4;  // (the streaming body batches its rounds the same way)
         const uint32_t eb6 = wst + 16u;
         // stream 1's u16 region (bytes; a multiple of 4 like eb6, so that every region's even
         // entries are dword-aligned for the flush)
@@ -1464,7 +1465,7 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
         // bases replicated into 4 bytes, merged by a uniform byte mask, plus the constant bytes
         // j — a byte-wise add with no carries between bytes (low 7 bits added, bit 7 xor-ed back)
         uint32_t pos6[4] = {0, 0, 0, 0};
-        if constexpr (E6) {
+        if constexpr (E6S) {
             const uint32_t A4 = perm(0u, pb0, 0x00000000u), B4 = perm(0u, pb1, 0x00000000u);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -1696,13 +1697,43 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
             };
             uint4 Tc;
             uint32_t Cc = chunk_of(0, load_group(gw0 + lane), Tc);
-            for (uint32_t r = 0; r < RW; ++r) {
-                uint4 Tn = make_uint4(0, 0, 0, 0);
-                uint32_t Cn = 0;
-                if (r + 1 < RW) Cn = chunk_of(r + 1, load_group(gw0 + (r + 1) * 64 + lane), Tn);
-                emit5(r, Tc, Cc);
-                Tc = Tn;
-                Cc = Cn;
+            if constexpr (E6S) {
+                // batches of rounds as in the resident body: a flush when the next round could
+                // overflow a stream's staging region, or at the wave's last round (a flush per
+                // round cost a 256 KiB message's waves 32 flushes instead of ~10)
+                const uint32_t cap6[2] = {1u + NB * 64u * Ls[0], 1u + NB * 64u * Ls[1]};
+                bool fresh = true;
+                uint32_t rb = 0;  // the batch's first round
+                for (uint32_t r = 0; r < RW; ++r) {
+                    uint4 Tn = make_uint4(0, 0, 0, 0);
+                    uint32_t Cn = 0;
+                    if (r + 1 < RW) Cn = chunk_of(r + 1, load_group(gw0 + (r + 1) * 64 + lane), Tn);
+                    if (fresh && lane == 0) {  // batch start: the pending entries
+                        if (hp[0]) *reinterpret_cast<uint16_t *>(smem + eb6) = (uint16_t)pend6[0];
+                        if (ns2 && hp[1]) *reinterpret_cast<uint16_t *>(smem + eb6 + eoff6) = (uint16_t)pend6[1];
+                    }
+                    fresh = false;
+                    sweep6(Tc, Cc);
+                    const bool over = (hp[0] ? 1u : 0u) + s6[0] + 64u * Ls[0] > cap6[0] ||
+                                      (ns2 && (hp[1] ? 1u : 0u) + s6[1] + 64u * Ls[1] > cap6[1]);
+                    if (over || r + 1 == RW) {
+                        const uint32_t gb = gw0 + rb * 64u, ge = gw0 + r * 64u + 64u;
+                        flush6(gb <= ngroups - 1 && ngroups - 1 < ge);
+                        fresh = true;
+                        rb = r + 1u;
+                    }
+                    Tc = Tn;
+                    Cc = Cn;
+                }
+            } else {
+                for (uint32_t r = 0; r < RW; ++r) {
+                    uint4 Tn = make_uint4(0, 0, 0, 0);
+                    uint32_t Cn = 0;
+                    if (r + 1 < RW) Cn = chunk_of(r + 1, load_group(gw0 + (r + 1) * 64 + lane), Tn);
+                    emit5(r, Tc, Cc);
+                    Tc = Tn;
+                    Cc = Cn;
+                }
             }
         }
         PSY_PROF_MARK(6);
