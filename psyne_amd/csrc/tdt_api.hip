@@ -223,6 +223,73 @@ int launch_encode_t(psy::EncodeArgs a, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------------------------------
+// Passthrough copies (UNCP): messages that stay UNCP (encode :227-266: below min_tensor_size, the
+// policy off, or a size that is not a whole number of words) and UNCP blobs (decode :271-304) get
+// a copy list of their own.  Sixteen lanes per entry, 16 entries per 256-lane workgroup,
+// grid-stride over the list (its length is device data); a one-wave team per 64-byte message
+// cost a whole wave's launch, LDS and header work.
+template <int GL>
+__device__ __forceinline__ void lanes_copy_any(uint8_t *dst, const uint8_t *src, uint64_t len, uint32_t l) {
+    // 16-byte aligned stores on dst; each 16-byte chunk read as aligned dwords and funnel-shifted
+    // by the source misalignment
+    uint64_t head = (16 - ((uintptr_t)dst & 15)) & 15;
+    if (head > len) head = len;
+    if (l < head) dst[l] = src[l];
+    const uint64_t nb = (len - head) / 16;
+    const uint8_t *s0 = src + head;
+    const uint32_t sh = (uint32_t)((uintptr_t)s0 & 3) * 8;
+    const uint32_t *sw = reinterpret_cast<const uint32_t *>((uintptr_t)s0 & ~(uintptr_t)3);
+    uint4 *dv = reinterpret_cast<uint4 *>(dst + head);
+    for (uint64_t k = l; k < nb; k += GL) {
+        const uint32_t *q = sw + 4 * k;
+        const uint32_t w0 = psy::gload<uint32_t>(q), w1 = psy::gload<uint32_t>(q + 1), w2 = psy::gload<uint32_t>(q + 2),
+                       w3 = psy::gload<uint32_t>(q + 3);
+        const uint32_t w4 = sh ? psy::gload<uint32_t>(q + 4) : 0u;  // (only when misaligned: inside src)
+        dv[k] = make_uint4((uint32_t)((((uint64_t)w1 << 32) | w0) >> sh), (uint32_t)((((uint64_t)w2 << 32) | w1) >> sh),
+                           (uint32_t)((((uint64_t)w3 << 32) | w2) >> sh), (uint32_t)((((uint64_t)w4 << 32) | w3) >> sh));
+    }
+    for (uint64_t k = head + 16 * nb + l; k < len; k += GL) dst[k] = src[k];
+}
+
+// encode: blob = "UNCP" + payload in the message's slot (slotted batches)
+__global__ __launch_bounds__(256) void tdt_encode_copy_kernel(psy::EncodeArgs a) {
+    const uint32_t n = __builtin_amdgcn_readfirstlane(*a.list_count);
+    const uint32_t q = threadIdx.x >> 4, l = threadIdx.x & 15u;
+    for (uint32_t i = blockIdx.x * 16u + q; i < n; i += gridDim.x * 16u) {
+        const uint32_t msg = a.list[i];
+        const uint64_t off0 = a.in_off[msg], len = a.in_off[msg + 1] - off0;
+        const uint64_t sb = a.slot_off[msg], E = len + 4;
+        const bool fits = E <= a.slot_off[msg + 1] - sb;
+        if (l == 0) {
+            if (a.status) a.status[msg] = fits ? psy::ST_OK : psy::ST_CAPACITY;
+            if (a.out_len) a.out_len[msg] = fits ? E : 0;
+        }
+        if (!fits) continue;
+        uint8_t *dst = a.out + sb;
+        if (l < 4) dst[l] = (uint8_t)(psy::kMagicUNCP >> (8 * l));
+        lanes_copy_any<16>(dst + 4, a.in + off0, len, l);
+    }
+}
+
+// decode: payload of a UNCP blob into its slot
+__global__ __launch_bounds__(256) void tdt_decode_copy_kernel(psy::DecodeArgs a) {
+    const uint32_t n = __builtin_amdgcn_readfirstlane(*a.list_count);
+    const uint32_t q = threadIdx.x >> 4, l = threadIdx.x & 15u;
+    for (uint32_t i = blockIdx.x * 16u + q; i < n; i += gridDim.x * 16u) {
+        const uint32_t msg = a.list[i];
+        const uint64_t boff = a.in_off[msg];
+        const uint64_t len = a.in_len ? a.in_len[msg] : a.in_off[msg + 1] - boff;  // >= 4 (the plan)
+        const uint64_t ob = a.slot_off[msg], osize = len - 4;
+        const bool fits = osize <= a.slot_off[msg + 1] - ob;
+        if (l == 0) {
+            if (a.out_len) a.out_len[msg] = fits ? osize : 0;
+            if (a.status) a.status[msg] = fits ? psy::ST_OK : psy::ST_CAPACITY;
+        }
+        if (fits) lanes_copy_any<16>(a.out + ob, a.in + boff + 4, osize, l);
+    }
+}
+
+// ---------------------------------------------------------------------------------------
 // Slotted encode (the hot path): a plan kernel sorts the messages into classes — large
 // messages as 64 KiB tiles (histogram + mapping, count, scan, emit), medium messages one
 // 512-lane team each, small ones one wave each — into lists whose lengths stay in device
@@ -259,7 +326,7 @@ uint32_t pow2_at_least(uint64_t x, uint32_t lo, uint32_t hi) {
 }
 
 int ensure_plan(PlanWS &w, uint32_t n, hipStream_t s) {
-    const size_t need = 256 + 16ull * n;  // counters | small | medium | mid-sized | big lists
+    const size_t need = 256 + 20ull * n;  // counters | small | medium | mid-sized | big | copy lists
     if (need > w.bytes) {
         if (int st = no_growth_in_capture(s)) return st;
         if (w.buf) HIPCHK(hipFree(w.buf));
@@ -363,6 +430,7 @@ int launch_slotted(tdt_ctx *c, PlanWS &pw, psy::EncodeArgs a, hipStream_t s) {
     // classes an earlier plan found empty are off (their messages, if any, go medium)
     const bool small_on = !H.valid || H.v[10] > 0;  // (counter 5: small messages, listed or not)
     const bool mid_on = !H.valid || H.v[14] > 0;    // (counter 7: mid-sized messages, listed or not)
+    const bool copy_on = !H.valid || H.v[18] > 0;   // (counter 9: UNCP messages)
     bool tiles_on = !H.valid || H.v[4] > 0;
     if (tiles_on && !capturing) {
         st = ensure_elarge(pw, WS, s);
@@ -372,7 +440,7 @@ int launch_slotted(tdt_ctx *c, PlanWS &pw, psy::EncodeArgs a, hipStream_t s) {
     auto *cnt64 = reinterpret_cast<unsigned long long *>(pw.buf);
     auto *cnt = reinterpret_cast<uint32_t *>(pw.buf);  // cnt[2k]: the low word of counter k
     uint32_t *slist = reinterpret_cast<uint32_t *>(pw.buf + 256), *mlist = slist + n, *qlist = mlist + n,
-             *blist = qlist + n;
+             *blist = qlist + n, *clist = blist + n;
     const uint32_t lcap = tiles_on ? pw.e_lcap : 0u;
     const uint32_t tcap = tiles_on ? std::min(pw.e_tcap, std::max(c->tile_cap, psy::kSpanTiles)) : 0u;
     const uint32_t scap = tcap / psy::kSpanTiles;
@@ -383,8 +451,10 @@ int launch_slotted(tdt_ctx *c, PlanWS &pw, psy::EncodeArgs a, hipStream_t s) {
         reinterpret_cast<uint64_t *>(reinterpret_cast<uint8_t *>(trec) + sizeof(psy::TileRec) * pw.e_tcap);
     auto *shist = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(spans) + 8ull * (pw.e_tcap / psy::kSpanTiles));
     HIPCHK(hipMemsetAsync(cnt, 0, 128, s));
-    psy::PlanArgs p{a.in_off,  n,    cnt64,     slist,   mlist,   qlist, blist, tiles, spans, lmeta, lcap, tcap,
-                    kSmallMax, kMidMax, kBigMin, c->large_min, small_on ? 1u : 0u, mid_on ? 1u : 0u};
+    psy::PlanArgs p{a.in_off,  n,       cnt64,   slist,          mlist,              qlist,
+                    blist,     clist,   tiles,   spans,          lmeta,              lcap,
+                    tcap,      kSmallMax, kMidMax, kBigMin,      c->large_min,       small_on ? 1u : 0u,
+                    mid_on ? 1u : 0u, a.min_tensor, (uint32_t)a.policy_on, (uint32_t)WS, copy_on ? 1u : 0u};
     const uint32_t per = psy::kPlanThreads * psy::kPlanPer;
     hipLaunchKernelGGL(psy::tdt_encode_plan_kernel, dim3((uint32_t)(((uint64_t)n + per - 1) / per)),
                        dim3(psy::kPlanThreads), 0, s, p);
@@ -402,7 +472,7 @@ int launch_slotted(tdt_ctx *c, PlanWS &pw, psy::EncodeArgs a, hipStream_t s) {
     // the side stream carries the tile pipeline and the small / mid-sized lists beside the medium
     // list (queued behind it on one stream they would run alone in its tail)
     const bool medium_on = !H.valid || H.v[2] + H.v[16] > 0;  // (counters 1 and 8)
-    if (tiles_on || ((small_on || mid_on) && medium_on && !c->small_main)) {
+    if (tiles_on || ((small_on || mid_on || copy_on) && medium_on && !c->small_main)) {
         const int fr = c->no_side ? -1 : fork_side(pw, s);
         if (fr > 0) return fr;
         forked = fr == TDT_OK;
@@ -476,6 +546,13 @@ int launch_slotted(tdt_ctx *c, PlanWS &pw, psy::EncodeArgs a, hipStream_t s) {
                                     ss, a);
              });
     }
+    // passthrough copies on the small list's stream
+    if (copy_on) {
+        a.list = clist;
+        a.list_count = cnt + 20;
+        hipLaunchKernelGGL(tdt_encode_copy_kernel, dim3(std::max(1u, std::min((uint32_t)c->cus * 8u, (n + 15) / 16))),
+                           dim3(256), 0, forked && !c->small_main ? pw.side : s, a);
+    }
     // mid-sized messages (256-lane teams) on the small list's stream
     if (mid_on) {
         const hipStream_t qs = forked && !c->small_main ? pw.side : s;
@@ -533,7 +610,7 @@ int launch_encode_ws(psy::EncodeArgs a, bool small, hipStream_t s) {
 bool lb_small_teams(tdt_ctx *c, hipStream_t s) {
     CountHist &H = c->pw.eh;
     if (!capturing(s)) H.refresh();
-    if (H.valid && H.n) return 2ull * H.v[10] > H.n;  // (counter 5: small messages)
+    if (H.valid && H.n) return 2ull * ((uint64_t)H.v[10] + H.v[18]) > H.n;  // (counters 5, 9: small, UNCP)
     return c->size_hint.load() <= kSmallMax;
 }
 
@@ -667,6 +744,7 @@ int launch_decode_slotted(tdt_ctx *c, PlanWS &pw, psy::DecodeArgs a, hipStream_t
     CountHist &H = pw.dh;
     if (!capturing) H.refresh();
     const bool small_on = !H.valid || H.v[10] > 0;  // counter 5: small blobs, listed or not
+    const bool copy_on = !H.valid || H.v[14] > 0;   // counter 7: UNCP blobs
     bool large_on = !H.valid || H.v[2] > 0;
     if (large_on && !capturing) {
         st = ensure_dlarge(pw, s);
@@ -676,15 +754,15 @@ int launch_decode_slotted(tdt_ctx *c, PlanWS &pw, psy::DecodeArgs a, hipStream_t
     auto *cnt = reinterpret_cast<unsigned long long *>(pw.buf);
     auto *cnt32 = reinterpret_cast<uint32_t *>(pw.buf);
     auto *list = reinterpret_cast<uint32_t *>(pw.buf + 256);
-    uint32_t *slist = list + n, *blist = slist + n;
+    uint32_t *slist = list + n, *blist = slist + n, *clist = blist + n;
     const uint32_t lcap = large_on ? pw.d_lcap : 0u, bcap = large_on ? pw.d_bcap : 0u,
                    tcap = large_on ? pw.d_tcap : 0u;
     auto *dmeta = reinterpret_cast<psy::DMeta *>(pw.dlarge);
     auto *bent = reinterpret_cast<uint32_t *>(pw.dlarge + (size_t)pw.d_lcap * sizeof(psy::DMeta));
     uint32_t *bsum = bent + pw.d_bcap, *tent = bsum + pw.d_bcap, *tblk = tent + pw.d_tcap;
     HIPCHK(hipMemsetAsync(cnt, 0, 128, s));
-    psy::DPlanArgs p{a.in, a.in_off, a.in_len, n, cnt, list, slist, kDSmallMax, blist, kDBigMin, dmeta, bent,
-                     tent, lcap, bcap, tcap, c->large_min, small_on ? 1u : 0u};
+    psy::DPlanArgs p{a.in, a.in_off, a.in_len, n, cnt, list, slist, kDSmallMax, blist, kDBigMin, clist, dmeta,
+                     bent, tent, lcap, bcap, tcap, c->large_min, small_on ? 1u : 0u, copy_on ? 1u : 0u};
     hipLaunchKernelGGL(psy::tdt_decode_plan_kernel, dim3((uint32_t)(((uint64_t)n + 4095) / 4096)), dim3(1024), 0, s, p);
     HIPCHK(hipGetLastError());
     if (!capturing && (st = record_counts(H, cnt, n, s))) return st;
@@ -714,7 +792,7 @@ int launch_decode_slotted(tdt_ctx *c, PlanWS &pw, psy::DecodeArgs a, hipStream_t
     // the side stream carries the large-blob pipeline and the small-blob list beside the main
     // list (the small list queued behind the main list ran alone in its tail: C4 1.6 ms)
     const bool main_on = !H.valid || H.v[0] + H.v[12] > 0;  // (counters 0 and 6)
-    if (large_on || (small_on && main_on && !c->small_main)) {
+    if (large_on || ((small_on || copy_on) && main_on && !c->small_main)) {
         const int fr = c->no_side ? -1 : fork_side(pw, s);
         if (fr > 0) return fr;
         forked = fr == TDT_OK;
@@ -743,6 +821,13 @@ int launch_decode_slotted(tdt_ctx *c, PlanWS &pw, psy::DecodeArgs a, hipStream_t
     const uint32_t gmain = H.valid ? std::min<uint32_t>(n, guess(H, 0, n, n) + guess(H, 12, n, n)) : n;
     lists(gmain, s, psy::tdt_decode_kernel<0, psy::kDecWR, 0>, psy::tdt_decode_kernel<0, psy::kDecWR, 1>);
     a.blist = nullptr;
+    // passthrough copies beside the main list
+    if (copy_on) {
+        a.list = clist;
+        a.list_count = cnt32 + 16;
+        hipLaunchKernelGGL(tdt_decode_copy_kernel, dim3(std::max(1u, std::min((uint32_t)c->cus * 8u, (n + 15) / 16))),
+                           dim3(256), 0, forked && !c->small_main ? pw.side : s, a);
+    }
     // small blobs: one-round windows (a third less LDS per wave: more blobs in flight per CU)
     if (small_on) {
         a.list = slist;

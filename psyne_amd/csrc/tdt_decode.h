@@ -1094,18 +1094,21 @@ struct DPlanArgs {
     uint32_t n_msgs;
     // [0] one-wave blobs, [1] large blobs, [2] tiles, [3] block slots, [4] small blobs (listed),
     // [5] small blobs (listed or not: the host's count history switches the small list back on),
-    // [6] big one-wave blobs (their own list, dispatched first)
+    // [6] big one-wave blobs (their own list, dispatched first), [7] UNCP blobs (listed or not),
+    // [8] UNCP blobs listed (the copy list)
     unsigned long long *cnt;
     uint32_t *list;
     uint32_t *slist;          // blobs decoding to <= small_max bytes (one-round windows: less LDS per wave)
     uint64_t small_max;
     uint32_t *blist;          // one-wave blobs decoding to > big_min bytes (dispatched first)
     uint64_t big_min;
+    uint32_t *clist;          // UNCP blobs (passthrough copies, several per wave)
     DMeta *dmeta;
     uint32_t *bent, *tent;
     uint32_t lmax, bcap, tcap;  // (0, 0, 0: no tiled path)
     uint64_t large_min;
     uint32_t small_on;  // 0: small blobs join the one-wave list
+    uint32_t copy_on;   // 0: UNCP blobs join the one-wave lists
 };
 
 __global__ __launch_bounds__(1024) void tdt_decode_plan_kernel(DPlanArgs p) {
@@ -1119,7 +1122,7 @@ __global__ __launch_bounds__(1024) void tdt_decode_plan_kernel(DPlanArgs p) {
         thr = share > thr ? share : thr;
     }
     uint64_t isl[4], nt[4], nb[4], j[4], t0[4], b0[4], one[4], pos[4], sm[4], spos[4], sc[4], scp[4], bg[4], bpos[4];
-    uint64_t osz_k[4];
+    uint64_t osz_k[4], unc[4] = {0, 0, 0, 0}, cpo[4], cpp[4], ucc[4], ucp[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const uint32_t i = (blockIdx.x * 4 + k) * 1024 + threadIdx.x;
@@ -1136,7 +1139,11 @@ __global__ __launch_bounds__(1024) void tdt_decode_plan_kernel(DPlanArgs p) {
                     nbs = len / 1024 + 3;  // >= the 512-pair blocks of <= 2 referenced streams
                 } else if (magic == kMagicUNCP) {
                     osz = len - 4;
+                    unc[k] = 1;
                 }
+            } else if (len >= 4 && ld_u32_bytes(p.in + boff) == kMagicUNCP) {
+                osz = len - 4;
+                unc[k] = 1;
             }
             osz_k[k] = osz;
             if (osz > thr) {
@@ -1169,7 +1176,11 @@ __global__ __launch_bounds__(1024) void tdt_decode_plan_kernel(DPlanArgs p) {
                 for (uint64_t b = b0[k]; b < b0[k] + nb[k] && b < p.bcap; ++b) p.bent[b] = kNone;
             }
         }
-        const bool any = i < p.n_msgs && !large;
+        const bool uncp = i < p.n_msgs && !large && !isl[k] && unc[k];
+        const bool copy = uncp && p.copy_on;
+        ucc[k] = uncp ? 1u : 0u;
+        cpo[k] = copy ? 1u : 0u;
+        const bool any = i < p.n_msgs && !large && !copy;
         const bool small = any && !isl[k] && p.small_max && osz_k[k] <= p.small_max;
         sc[k] = small ? 1u : 0u;
         sm[k] = small && p.small_on ? 1u : 0u;
@@ -1181,11 +1192,14 @@ __global__ __launch_bounds__(1024) void tdt_decode_plan_kernel(DPlanArgs p) {
     wg_claim<4>(sm, spos, p.cnt + 4, lds);
     wg_claim<4>(sc, scp, p.cnt + 5, lds);
     wg_claim<4>(bg, bpos, p.cnt + 6, lds);
+    wg_claim<4>(ucc, ucp, p.cnt + 7, lds);
+    wg_claim<4>(cpo, cpp, p.cnt + 8, lds);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         if (one[k]) p.list[pos[k]] = (blockIdx.x * 4 + k) * 1024 + threadIdx.x;
         if (sm[k]) p.slist[spos[k]] = (blockIdx.x * 4 + k) * 1024 + threadIdx.x;
         if (bg[k]) p.blist[bpos[k]] = (blockIdx.x * 4 + k) * 1024 + threadIdx.x;
+        if (cpo[k]) p.clist[cpp[k]] = (blockIdx.x * 4 + k) * 1024 + threadIdx.x;
     }
 }
 

@@ -1816,15 +1816,21 @@ struct PlanArgs {
     // [0] small (listed), [1] medium, [2] large entries, [3] tiles, [4] spans claimed, [5] small
     // messages (listed or not: the host's count history switches the small class back on), [6]
     // mid-sized (listed), [7] mid-sized messages (listed or not), [8] medium messages over big_min
-    // (their own list, dispatched first)
+    // (their own list, dispatched first), [9] passthrough (UNCP) messages up to large_min (listed or
+    // not), [10] UNCP messages listed
     unsigned long long *cnt;
-    uint32_t *slist, *mlist, *qlist, *blist;
+    uint32_t *slist, *mlist, *qlist, *blist, *clist;
     uint64_t *tiles, *spans;
     LMeta *lmeta;
     uint32_t lmax, tile_cap;  // span_cap = tile_cap / kSpanTiles (0, 0: no tiled path)
     uint64_t small_max, mid_max, big_min, large_min;
     uint32_t small_on;  // 0: small messages join the medium list
     uint32_t mid_on;    // 0: mid-sized messages join the medium list
+    // should_transform :186-201 + compress_tdt's size guard :364-367, as encode_one evaluates
+    // them: messages that stay UNCP go to the copy list (clist null: no copy list)
+    uint64_t min_tensor;
+    uint32_t policy_on, ws;
+    uint32_t copy_on;  // 0: UNCP messages join their size classes (the count history switches it on)
 };
 
 constexpr uint32_t kPlanThreads = 1024, kPlanPer = 2;  // messages per plan workgroup: 2048
@@ -1846,7 +1852,8 @@ __global__ __launch_bounds__(kPlanThreads) void tdt_encode_plan_kernel(PlanArgs 
     wg_claim<kPlanPer>(T, t0, p.cnt + 3, lds);
     wg_claim<kPlanPer>(S, s0, p.cnt + 4, lds);
     uint64_t sm[kPlanPer], md[kPlanPer], ps[kPlanPer], pm[kPlanPer], sc[kPlanPer], pc[kPlanPer];
-    uint64_t qm[kPlanPer], pq[kPlanPer], qc[kPlanPer], pqc[kPlanPer], bm[kPlanPer], pb[kPlanPer];
+    uint64_t qm[kPlanPer], pq[kPlanPer], qc[kPlanPer], pqc[kPlanPer], bm[kPlanPer], pb[kPlanPer], cp[kPlanPer],
+        pcp[kPlanPer], cc[kPlanPer], pcc[kPlanPer];
 #pragma unroll
     for (int k = 0; k < (int)kPlanPer; ++k) {
         const uint32_t i = (blockIdx.x * kPlanPer + k) * kPlanThreads + threadIdx.x;
@@ -1870,13 +1877,19 @@ __global__ __launch_bounds__(kPlanThreads) void tdt_encode_plan_kernel(PlanArgs 
                 p.spans[s0[k] + t] = large ? (t << 32 | j[k]) : (uint64_t)kNone;
         }
         const bool valid = i < p.n_msgs;
-        const bool small = valid && !isl[k] && n[k] <= p.small_max;
-        const bool mid = valid && !isl[k] && !small && n[k] <= p.mid_max;
+        const bool transform = p.policy_on && n[k] >= p.min_tensor && (n[k] % 4 == 0) && n[k] >= 64 &&
+                               (n[k] % p.ws == 0) && n[k] < (1ull << 32);
+        const bool uncp = valid && !isl[k] && !transform;
+        const bool copy = uncp && p.copy_on;
+        cc[k] = uncp ? 1u : 0u;
+        cp[k] = copy ? 1u : 0u;
+        const bool small = valid && !isl[k] && !copy && n[k] <= p.small_max;
+        const bool mid = valid && !isl[k] && !copy && !small && n[k] <= p.mid_max;
         sc[k] = small ? 1u : 0u;
         sm[k] = small && p.small_on ? 1u : 0u;
         qc[k] = mid ? 1u : 0u;
         qm[k] = mid && p.mid_on ? 1u : 0u;
-        const bool medium = valid && !large && !sm[k] && !qm[k];
+        const bool medium = valid && !large && !copy && !sm[k] && !qm[k];
         bm[k] = medium && p.blist && n[k] > p.big_min ? 1u : 0u;
         md[k] = medium && !bm[k] ? 1u : 0u;
     }
@@ -1886,6 +1899,8 @@ __global__ __launch_bounds__(kPlanThreads) void tdt_encode_plan_kernel(PlanArgs 
     wg_claim<kPlanPer>(qm, pq, p.cnt + 6, lds);
     wg_claim<kPlanPer>(qc, pqc, p.cnt + 7, lds);
     wg_claim<kPlanPer>(bm, pb, p.cnt + 8, lds);
+    wg_claim<kPlanPer>(cc, pcc, p.cnt + 9, lds);
+    wg_claim<kPlanPer>(cp, pcp, p.cnt + 10, lds);
 #pragma unroll
     for (int k = 0; k < (int)kPlanPer; ++k) {
         const uint32_t i = (blockIdx.x * kPlanPer + k) * kPlanThreads + threadIdx.x;
@@ -1893,6 +1908,7 @@ __global__ __launch_bounds__(kPlanThreads) void tdt_encode_plan_kernel(PlanArgs 
         if (md[k]) p.mlist[pm[k]] = i;
         if (qm[k]) p.qlist[pq[k]] = i;
         if (bm[k]) p.blist[pb[k]] = i;
+        if (cp[k]) p.clist[pcp[k]] = i;
     }
 }
 
