@@ -182,6 +182,7 @@ struct tdt_ctx {
     bool no_side = false;       // PSYNE_TDT_NO_SIDE: no side stream for the tile pipeline
     bool small_main = false;    // PSYNE_TDT_SMALL_MAIN: small lists on the caller's stream
     bool no_two_phase = false;  // PSYNE_TDT_NO_TWO_PHASE: compacted calls take the one-pass kernels
+    uint32_t copy_wgs = 8;      // PSYNE_TDT_COPY_WGS: copy-list workgroups per CU
     int cus = 256;              // compute units (overflow grids)
 };
 
@@ -550,7 +551,7 @@ int launch_slotted(tdt_ctx *c, PlanWS &pw, psy::EncodeArgs a, hipStream_t s) {
     if (copy_on) {
         a.list = clist;
         a.list_count = cnt + 20;
-        hipLaunchKernelGGL(tdt_encode_copy_kernel, dim3(std::max(1u, std::min((uint32_t)c->cus * 8u, (n + 15) / 16))),
+        hipLaunchKernelGGL(tdt_encode_copy_kernel, dim3(std::max(1u, std::min((uint32_t)c->cus * c->copy_wgs, (n + 15) / 16))),
                            dim3(256), 0, forked && !c->small_main ? pw.side : s, a);
     }
     // mid-sized messages (256-lane teams) on the small list's stream
@@ -825,7 +826,7 @@ int launch_decode_slotted(tdt_ctx *c, PlanWS &pw, psy::DecodeArgs a, hipStream_t
     if (copy_on) {
         a.list = clist;
         a.list_count = cnt32 + 16;
-        hipLaunchKernelGGL(tdt_decode_copy_kernel, dim3(std::max(1u, std::min((uint32_t)c->cus * 8u, (n + 15) / 16))),
+        hipLaunchKernelGGL(tdt_decode_copy_kernel, dim3(std::max(1u, std::min((uint32_t)c->cus * c->copy_wgs, (n + 15) / 16))),
                            dim3(256), 0, forked && !c->small_main ? pw.side : s, a);
     }
     // small blobs: one-round windows (a third less LDS per wave: more blobs in flight per CU)
@@ -1347,6 +1348,7 @@ int tdt_ctx_create(int device, const tdt_config *cfg, tdt_ctx **out) {
     x->no_side = flag("PSYNE_TDT_NO_SIDE");
     x->small_main = flag("PSYNE_TDT_SMALL_MAIN");
     x->no_two_phase = flag("PSYNE_TDT_NO_TWO_PHASE");
+    if (const char *e = std::getenv("PSYNE_TDT_COPY_WGS")) x->copy_wgs = std::max(1ul, std::strtoul(e, nullptr, 10));
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
         x->cus = cus;
