@@ -26,6 +26,9 @@ rc=$?; [ $rc -eq 0 ] || exit $rc
 python3 tools/prof_summary.py "$OUT/prof" "$OUT/kernel_stats.md" "rocprofv3 --kernel-trace --stats: bench.py --steps 5 --warmup 2 ($TAG)" --steady 5 > /dev/null
 step pmc
 bash tools/profile_pmc.sh "$OUT/pmc" || exit 1
+step pmc_c2_c4
+PMC_KEY=c2_1048576x1024 bash tools/profile_pmc.sh "$OUT/pmc_c2" --workload c2 --steps 1 --warmup 1 --cpu-seconds 0 --compacted-steps 0 || exit 1
+PMC_KEY=c4_4194304x65536 bash tools/profile_pmc.sh "$OUT/pmc_c4" --workload c4 --steps 1 --warmup 1 --cpu-seconds 0 --compacted-steps 0 || exit 1
 step c2_c4
 for wl in c2 c4; do
   timeout -k 10 400 python -u bench.py --workload $wl --steps 5 --warmup 2 --cpu-seconds 0 > "$OUT/bench_$wl.log" 2>&1
