@@ -187,6 +187,7 @@ struct tdt_ctx {
     // list on the side stream (C4 decode 11.80 -> 11.42 ms at 8 KiB against 1 KiB; 16-64 KiB
     // gave 11.6-11.8, profiles/r03_dsm2/ab.txt)
     uint64_t dsmall_max = 8192;
+    uint64_t dbig_min = 128 * 1024;  // PSYNE_TDT_DBIG_MIN: one-wave blobs above this are dispatched first
     int cus = 256;              // compute units (overflow grids)
 };
 
@@ -713,7 +714,6 @@ int encode_common(tdt_ctx *c, int mode, const uint8_t *d_in, const uint64_t *d_i
 // the device: main grids from an earlier call's counts, overflow launches past them.
 constexpr uint32_t kDLmax = 1u << 16, kDBcap = 1u << 23, kDTcap = 1u << 20;  // full budgets
 constexpr uint32_t kDL0 = 1024, kDB0 = 1u << 16, kDT0 = 8192;                 // starting budgets
-constexpr uint64_t kDBigMin = 128 * 1024;  // one-wave blobs above this are dispatched first
 size_t dlarge_bytes(uint32_t lcap, uint32_t bcap, uint32_t tcap) {
     return (size_t)lcap * sizeof(psy::DMeta) + 8ull * bcap + 4ull * tcap + 8ull * tcap;
 }
@@ -765,7 +765,7 @@ int launch_decode_slotted(tdt_ctx *c, PlanWS &pw, psy::DecodeArgs a, hipStream_t
     auto *bent = reinterpret_cast<uint32_t *>(pw.dlarge + (size_t)pw.d_lcap * sizeof(psy::DMeta));
     uint32_t *bsum = bent + pw.d_bcap, *tent = bsum + pw.d_bcap, *tblk = tent + pw.d_tcap;
     HIPCHK(hipMemsetAsync(cnt, 0, 128, s));
-    psy::DPlanArgs p{a.in, a.in_off, a.in_len, n, cnt, list, slist, c->dsmall_max, blist, kDBigMin, clist, dmeta,
+    psy::DPlanArgs p{a.in, a.in_off, a.in_len, n, cnt, list, slist, c->dsmall_max, blist, c->dbig_min, clist, dmeta,
                      bent, tent, lcap, bcap, tcap, c->large_min, small_on ? 1u : 0u, copy_on ? 1u : 0u};
     hipLaunchKernelGGL(psy::tdt_decode_plan_kernel, dim3((uint32_t)(((uint64_t)n + 4095) / 4096)), dim3(1024), 0, s, p);
     HIPCHK(hipGetLastError());
@@ -1351,6 +1351,7 @@ int tdt_ctx_create(int device, const tdt_config *cfg, tdt_ctx **out) {
     x->no_side = flag("PSYNE_TDT_NO_SIDE");
     x->small_main = flag("PSYNE_TDT_SMALL_MAIN");
     x->no_two_phase = flag("PSYNE_TDT_NO_TWO_PHASE");
+    if (const char *e = std::getenv("PSYNE_TDT_DBIG_MIN")) x->dbig_min = std::strtoull(e, nullptr, 10);
     if (const char *e = std::getenv("PSYNE_TDT_DSMALL_MAX")) x->dsmall_max = std::strtoull(e, nullptr, 10);
     if (const char *e = std::getenv("PSYNE_TDT_COPY_WGS")) x->copy_wgs = std::max(1ul, std::strtoul(e, nullptr, 10));
     int cus = 0;
