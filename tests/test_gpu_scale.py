@@ -70,6 +70,41 @@ def test_c2_full_batch_bitexact():
     check_slotted(make_codec(), data, off)
 
 
+@pytest.mark.timeout(900)
+def test_c3_full_batch_bitexact():
+    """The headline batch (BASELINE configs[2], bench.py's default): 262,144 x 64 KiB
+    gradient-like float32 messages generated on the device as bench.py does (seed 0x5EED0002),
+    16 GiB; every blob of the slotted encode compared byte for byte with the oracle's (chunks of
+    8,192 messages), then the whole batch decoded back on the device."""
+    import bench
+    n, mb = 262144, 65536
+    data = bench.gen_gradient(torch, n, mb, 0x5EED0002, torch.device("cuda"))
+    off = torch.arange(n + 1, dtype=torch.int64, device="cuda") * mb
+    codec = make_codec()
+    out, slots, lens, st = codec.encode_into(data, off)
+    torch.cuda.synchronize()
+    assert int(st[:n].abs().sum()) == 0
+    orc = Oracle()
+    sl = slots.cpu().numpy().astype(np.int64)
+    ln = lens[:n].cpu().numpy().astype(np.int64)
+    chunk = 8192
+    for c0 in range(0, n, chunk):
+        c1 = min(n, c0 + chunk)
+        host = data[c0 * mb:c1 * mb].cpu().numpy()
+        want, wslot, wlen = orc.encode_slotted(host, np.arange(c1 - c0 + 1, dtype=np.uint64) * mb, bandwidth=10.0)
+        assert np.array_equal(ln[c0:c1], wlen.astype(np.int64)), "blob lengths differ in chunk %d" % c0
+        got = out[int(sl[c0]):int(sl[c1])].cpu().numpy()
+        gs = sl[c0:c1] - sl[c0]
+        ws = wslot.astype(np.int64)
+        for i in range(c1 - c0):
+            L, a, b = int(ln[c0 + i]), int(gs[i]), int(ws[i])
+            assert np.array_equal(got[a:a + L], want[b:b + L]), "blob %d differs" % (c0 + i)
+    back, dsl, dln, dst = codec.decode_into(out, slots, in_lengths=lens)
+    torch.cuda.synchronize()
+    assert int(dst[:n].abs().sum()) == 0
+    assert torch.equal(back[:n * mb], data)
+
+
 @pytest.mark.timeout(600)
 def test_c4_zipf_full_range_bitexact():
     """C4's size distribution over its FULL range (bench.zipf_sizes: 64 B - 1 MiB, Zipf(1.5),
