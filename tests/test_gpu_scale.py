@@ -105,6 +105,44 @@ def test_c3_full_batch_bitexact():
     assert torch.equal(back[:n * mb], data)
 
 
+@pytest.mark.timeout(900)
+def test_c4_full_batch_bitexact():
+    """The C4 bench batch itself (bench.py --workload c4): 4 Mi messages of Zipf(1.5) sizes
+    64 B - 1 MiB (24.6 GiB, every message class), gradient-like data from the bench's generator
+    and seed; every blob byte for byte against the oracle (chunks of 262,144 messages, blob by
+    blob), then the whole batch decoded back on the device."""
+    import bench
+    sizes = bench.zipf_sizes(1 << 22, 0x5EED0003)
+    off = np.zeros(sizes.size + 1, np.int64)
+    off[1:] = np.cumsum(sizes)
+    data = bench.gen_gradient(torch, 1, int(off[-1]), 0x5EED0003, torch.device("cuda"))
+    n = sizes.size
+    codec = make_codec()
+    doff = torch.from_numpy(off).cuda()
+    out, slots, lens, st = codec.encode_into(data, doff)
+    torch.cuda.synchronize()
+    assert int(st[:n].abs().sum()) == 0
+    orc = Oracle()
+    sl = slots.cpu().numpy().astype(np.int64)
+    ln = lens[:n].cpu().numpy().astype(np.int64)
+    chunk = 262144
+    for c0 in range(0, n, chunk):
+        c1 = min(n, c0 + chunk)
+        host = data[int(off[c0]):int(off[c1])].cpu().numpy()
+        want, wslot, wlen = orc.encode_slotted(host, (off[c0:c1 + 1] - off[c0]).astype(np.uint64), bandwidth=10.0)
+        assert np.array_equal(ln[c0:c1], wlen.astype(np.int64)), "blob lengths differ in chunk %d" % c0
+        got = out[int(sl[c0]):int(sl[c1])].cpu().numpy()
+        gs = sl[c0:c1] - sl[c0]
+        ws = wslot.astype(np.int64)
+        for i in range(c1 - c0):
+            L, a, b = int(ln[c0 + i]), int(gs[i]), int(ws[i])
+            assert np.array_equal(got[a:a + L], want[b:b + L]), "blob %d differs" % (c0 + i)
+    back, dsl, dln, dst = codec.decode_into(out, slots, in_lengths=lens)
+    torch.cuda.synchronize()
+    assert int(dst[:n].abs().sum()) == 0
+    assert torch.equal(back[:int(off[-1])], data)
+
+
 @pytest.mark.timeout(600)
 def test_c4_zipf_full_range_bitexact():
     """C4's size distribution over its FULL range (bench.zipf_sizes: 64 B - 1 MiB, Zipf(1.5),
