@@ -1,5 +1,6 @@
 """GPU parity at BASELINE sizes: the HIP codec through the C ABI against
-the C oracle (pinned by tests/golden/) on the full C2 batch, on 100 k mixed messages, and on
+the C oracle (pinned by tests/golden/) on the full C2, C3 and C4 bench batches, on 100 k mixed
+messages, and on
 single messages up to SimpleTCP's 100 MB frame cap (tcp_simple.hpp:127-134) at several
 alignments.  Bit-exact: byte/integer work with a bit-exact restated entropy decision."""
 import numpy as np
