@@ -59,7 +59,8 @@ def parse():
     ap.add_argument("--msg-bytes", type=int, default=65536)
     ap.add_argument("--cpu-seconds", type=float, default=3.0,
                     help="target duration of EACH of the four CPU-baseline rows (0 = skip)")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = all usable host cores")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="threads of the all-cores CPU baseline row (0 = one per physical core of the host)")
     ap.add_argument("--cpu-kind", choices=["reference", "port"], default="reference")
     ap.add_argument("--host-inclusive", action="store_true",
                     help="also time host buffers (pinned and pageable) through H2D+kernel+D2H")
@@ -97,14 +98,76 @@ def free_port() -> int:
     return p
 
 
+def visible_gpus() -> list:
+    """The GPUs this process may use, found WITHOUT touching HIP (no torch, no HIP runtime: the
+    launcher parent must never initialise the GPU): KFD topology nodes with SIMDs
+    (/sys/class/kfd/kfd/topology/nodes/*/properties), in node order (the HIP device order),
+    narrowed by ROCR_VISIBLE_DEVICES, then HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES.  Each entry
+    is that node's properties (drm_render_minor, location_id, ...)."""
+    root = pathlib.Path("/sys/class/kfd/kfd/topology/nodes")
+    gpus = []
+    try:
+        for d in sorted(root.iterdir(), key=lambda q: int(q.name) if q.name.isdigit() else 1 << 30):
+            props = {}
+            for line in (d / "properties").read_text().splitlines():
+                f = line.split()
+                if len(f) == 2 and f[1].lstrip("-").isdigit():
+                    props[f[0]] = int(f[1])
+            if props.get("simd_count", 0) > 0:
+                gpus.append(props)
+    except (OSError, ValueError):
+        return []
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None and v.strip() != "":
+            idx = [int(x) for x in v.split(",") if x.strip().isdigit()]
+            gpus = [gpus[i] for i in idx if 0 <= i < len(gpus)]
+    return gpus
+
+
+def parse_cpulist(text: str) -> set:
+    cpus = set()
+    for part in text.strip().split(","):
+        if not part:
+            continue
+        lo, _, hi = part.partition("-")
+        cpus.update(range(int(lo), int(hi or lo) + 1))
+    return cpus
+
+
+def numa_bind(local_rank: int):
+    """Bind this rank's threads to the NUMA node of its GPU's PCIe root (before its first GPU
+    call), so that its pinned staging and host threads are node-local.  Returns what was done
+    (None: no topology information)."""
+    gpus = visible_gpus()
+    if local_rank >= len(gpus) or "drm_render_minor" not in gpus[local_rank]:
+        return None
+    minor = gpus[local_rank]["drm_render_minor"]
+    try:
+        node = int(pathlib.Path("/sys/class/drm/renderD%d/device/numa_node" % minor).read_text())
+    except (OSError, ValueError):
+        return None
+    if node < 0:
+        return {"numa_node": node, "bound": False}
+    try:
+        cpus = parse_cpulist(pathlib.Path("/sys/devices/system/node/node%d/cpulist" % node).read_text())
+        allowed = os.sched_getaffinity(0) & cpus
+        if not allowed:
+            return {"numa_node": node, "bound": False}
+        os.sched_setaffinity(0, allowed)
+    except OSError:
+        return {"numa_node": node, "bound": False}
+    return {"numa_node": node, "bound": True, "cpus": len(allowed)}
+
+
 def launch_ranks(a) -> int:
     """`bench.py --gpus N` outside a torch.distributed launch: start N ranks (one process per GPU)
-    as a child `torch.distributed.run` BEFORE this process touches the GPU, relay its output and
-    return its exit code.  (The child ranks see WORLD_SIZE == N and run main().)"""
+    as a child `torch.distributed.run` and relay its exit code.  This parent never touches HIP:
+    it counts GPUs from the KFD topology (visible_gpus) and imports neither torch nor the codec.
+    (The child ranks see WORLD_SIZE == N and run main().)"""
     shared = os.environ.get("PSYNE_BENCH_SHARED_DEVICE") == "1"
     if not shared:
-        import torch  # device_count() does not initialise the GPU on this image
-        have = torch.cuda.device_count()
+        have = len(visible_gpus())
         if have < a.gpus:
             print("bench.py: --gpus %d but only %d visible GPU(s)" % (a.gpus, have), file=sys.stderr, flush=True)
             return 2
@@ -201,12 +264,33 @@ def affinity_desc():
     return len(cpus), ",".join(runs)
 
 
+def physical_core_cpus():
+    """One logical CPU per physical core (lscpu's CORE,SOCKET pairs), within this process's
+    affinity: the pinning list of the all-cores CPU baseline."""
+    allowed = os.sched_getaffinity(0)
+    try:
+        out = subprocess.run(["lscpu", "-p=CPU,CORE,SOCKET"], capture_output=True, text=True, timeout=20).stdout
+    except Exception:
+        return sorted(allowed)
+    first = {}
+    for line in out.splitlines():
+        if not line or line.startswith("#"):
+            continue
+        f = line.split(",")
+        cpu, key = int(f[0]), (f[1], f[2])
+        if cpu in allowed and key not in first:
+            first[key] = cpu
+    return sorted(first.values()) or sorted(allowed)
+
+
 def cpu_baseline(data_u8, msg_bytes, target_s, threads, kind):
     """CPU rows of the REFERENCE codec (oracle/_ref, the reference header compiled where it lies)
-    on bounded samples of the same messages: {1, `threads`} threads x sample_fraction {0.3
-    (reference default), 1.0 (parity mode)}; one protocol object per thread.  The multi-thread
-    rows run over 4 GiB of DISTINCT messages (one pass: no cache-resident working set); the
-    1-thread rows over as many distinct messages as take about `target_s`."""
+    on bounded samples of the same messages, sample_fraction 0.3 (reference default) and 1.0
+    (parity mode), one protocol object per thread: 1 thread, and `threads` workers pinned one per
+    physical core (default: every physical core of the host); plus a 16-thread
+    row (the one-GPU box's CPU share).  The multi-thread rows run over 4 GiB of DISTINCT messages
+    (no cache-resident working set), repeated to last about 2 s; the 1-thread rows over as many
+    distinct messages as take about `target_s`."""
     import numpy as np
     from oracle.oracle import Oracle, Reference
     n_all = data_u8.numel() // msg_bytes
@@ -222,25 +306,34 @@ def cpu_baseline(data_u8, msg_bytes, target_s, threads, kind):
                                "build it in the container that has /root/reference (make -C oracle) or pass "
                                "--cpu-kind port")
         ref = Reference()
+        cores = physical_core_cpus()
+        if threads <= 0:
+            threads = len(cores)
+        pins = [cores[i % len(cores)] for i in range(threads)] if ref.has_pinned else None
         for sf in (0.3, 1.0):
             t1, _ = ref.bench(sample[: 16 * msg_bytes], off[:17], sample_fraction=sf, threads=1, reps=1)
             per_msg = t1 / 16
-            for thr in (1, threads):
-                k = n_big if thr > 1 else int(min(n_big, max(16, target_s / per_msg)))
-                secs, enc = ref.bench(sample[: k * msg_bytes], off[: k + 1], sample_fraction=sf, threads=thr, reps=1)
-                payload = k * msg_bytes
+            for thr in ((1, 16, threads) if sf == 0.3 else (1, threads)):
+                if thr > 1:
+                    k = n_big
+                    reps = int(min(8, max(1, -(-2.0 // (k * per_msg / thr)))))
+                    cp = pins if thr == threads else ([cores[i % len(cores)] for i in range(thr)] if pins else None)
+                else:
+                    k = int(min(n_big, max(16, target_s / per_msg)))
+                    reps, cp = 1, None
+                secs, enc = ref.bench(sample[: k * msg_bytes], off[: k + 1], sample_fraction=sf, threads=thr,
+                                      reps=reps, cpus=cp)
+                payload = k * msg_bytes * reps
                 rows.append(dict(value=payload / secs / 2**30, unit="GiB/s", cores=thr, sample_fraction=sf,
-                                 seconds=round(secs, 2), msgs=k, distinct_bytes=payload, ratio=float(payload / enc)))
+                                 seconds=round(secs, 2), msgs=k, reps=reps, distinct_bytes=k * msg_bytes,
+                                 pinned=cp is not None, ratio=float(payload / enc)))
         main = next(r for r in rows if r["sample_fraction"] == 0.3 and r["cores"] == threads)
         return dict(value=main["value"], unit="GiB/s", cores=threads, kind="reference",
-                    sample="%d distinct x %d B messages (the benched payload's first %.1f GiB, one pass), reference "
-                           "TDTCompressionProtocol encode+decode, default TDTConfig (sample_fraction 0.3), one "
-                           "object per thread, %d threads, %.1f s" % (main["msgs"], msg_bytes,
-                                                                      main["distinct_bytes"] / 2**30, threads,
-                                                                      main["seconds"]),
-                    rows=rows, nproc=nproc, lscpu_physical_cores=phys, affinity_cpus=aff_n, affinity_mask=aff,
-                    threads_note="threads = this process's affinity (%d CPUs: %s) capped by OMP_NUM_THREADS; "
-                                 "the host has %s physical cores" % (aff_n, aff, phys))
+                    sample="%d x %d B distinct msgs (first %.1f GiB of the payload) x %d passes; reference "
+                           "encode+decode, sample_fraction 0.3, one object per thread, %d threads pinned one per "
+                           "physical core, %.1f s" % (main["msgs"], msg_bytes, main["distinct_bytes"] / 2**30,
+                                                     main["reps"], threads, main["seconds"]),
+                    rows=rows, nproc=nproc, lscpu_physical_cores=phys, affinity_cpus=aff_n, affinity_mask=aff)
     orc = Oracle()
     t0 = time.perf_counter()
     k = 0
@@ -406,11 +499,15 @@ def main():
     if world != a.gpus:
         print("bench.py: --gpus %d but WORLD_SIZE=%d" % (a.gpus, world), file=sys.stderr, flush=True)
         sys.exit(2)
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # before the first GPU call: this rank's threads on its GPU's NUMA node (pinned staging and
+    # copy threads node-local)
+    orig_affinity = os.sched_getaffinity(0)
+    numa = None if os.environ.get("PSYNE_BENCH_SHARED_DEVICE") == "1" else numa_bind(local)
     import torch
     import torch.distributed as dist
 
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     # PSYNE_BENCH_SHARED_DEVICE=1: rehearsal of the N-rank path on a one-GPU box (every rank on
     # device 0, gloo for the barrier and reductions); never used for a reported number
     shared = os.environ.get("PSYNE_BENCH_SHARED_DEVICE") == "1"
@@ -564,7 +661,7 @@ def main():
         host = host_inclusive(torch, codec, data, off, n, mb)
         host["pcie_ceiling"] = pcie_ceiling(torch, dev)
     latency = message_latency(torch, codec, data) if a.latency and rank == 0 else None
-    per_rank = gather_obj({"rank": rank, "device": my_dev, "msgs": n, "payload_bytes": payload,
+    per_rank = gather_obj({"rank": rank, "device": my_dev, "numa": numa, "msgs": n, "payload_bytes": payload,
                            "GiBps": round(my_rate, 3), "kernels_ms": [round(t_enc, 4), round(t_dec, 4)],
                            "host_inclusive": host}, world)
 
@@ -579,8 +676,9 @@ def main():
         traffic = tr["kernels"][dom].get("hbm_bytes_per_launch") if tr and dom in tr.get("kernels", {}) else None
         cpu = None
         if a.cpu_seconds > 0 and a.workload == "c3" and world == 1:  # rank 0 at N=1 only
-            thr = a.cpu_threads or min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "1024")))
-            cpu = cpu_baseline(data, mb, a.cpu_seconds, thr, a.cpu_kind)
+            if orig_affinity:
+                os.sched_setaffinity(0, orig_affinity)  # the whole host, not the GPU's NUMA node
+            cpu = cpu_baseline(data, mb, a.cpu_seconds, a.cpu_threads, a.cpu_kind)
         if a.workload == "c3":
             metric = "TDT encode+decode GiB/s (device-resident), 64 KiB msgs, 1/2/4/8 MI355X"
             workload = "C3: %d x %d B float32 gradient-like messages per GPU, encode+decode" % (n, mb)

@@ -183,6 +183,11 @@ class Reference:
                                            C.POINTER(C.c_double), C.POINTER(C.c_int)]
         L.tdt_ref_bench.restype = C.c_double
         L.tdt_ref_bench.argtypes = [_u8p, _u64p, C.c_uint32, C.c_float, C.c_int, C.c_int, C.c_int, _u64p]
+        self.has_pinned = hasattr(L, "tdt_ref_bench_pinned")
+        if self.has_pinned:
+            L.tdt_ref_bench_pinned.restype = C.c_double
+            L.tdt_ref_bench_pinned.argtypes = [_u8p, _u64p, C.c_uint32, C.c_float, C.c_int, C.c_int, C.c_int, _u64p,
+                                               _i32p]
 
     @staticmethod
     def available(path=None) -> bool:
@@ -225,12 +230,23 @@ class Reference:
         return bool(self.lib.tdt_ref_should_transform(_ptr(d), n, word_size, bandwidth, cpu, min_tensor_size))
 
     def bench(self, data: np.ndarray, offsets: np.ndarray, sample_fraction=0.3, word_size=4,
-              threads=1, reps=1) -> tuple[float, int]:
+              threads=1, reps=1, cpus=None) -> tuple[float, int]:
+        """Wall seconds of `threads` workers (one protocol object each) encoding + decoding every
+        message `reps` times; cpus: one CPU per worker to pin it to (None: unpinned)."""
         d = _bytes(data)
         off = np.ascontiguousarray(offsets, dtype=np.uint64)
         enc = C.c_uint64(0)
-        s = self.lib.tdt_ref_bench(_ptr(d), _ptr(off, _u64p), len(off) - 1, sample_fraction, word_size,
-                                   threads, reps, C.byref(enc))
+        if cpus is not None:
+            if not self.has_pinned:
+                raise RuntimeError("oracle/_ref/libtdt_ref.so predates tdt_ref_bench_pinned: make -C oracle ref")
+            cp = np.ascontiguousarray(cpus, dtype=np.int32)
+            if cp.size != threads:
+                raise ValueError("one CPU per thread")
+            s = self.lib.tdt_ref_bench_pinned(_ptr(d), _ptr(off, _u64p), len(off) - 1, sample_fraction, word_size,
+                                              threads, reps, C.byref(enc), _ptr(cp, _i32p))
+        else:
+            s = self.lib.tdt_ref_bench(_ptr(d), _ptr(off, _u64p), len(off) - 1, sample_fraction, word_size,
+                                       threads, reps, C.byref(enc))
         if s < 0:
             raise RuntimeError("reference round trip mismatch in bench")
         return s, enc.value

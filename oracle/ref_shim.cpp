@@ -18,6 +18,9 @@
 #include <functional>
 #include <psyne/protocol/tdt_compression.hpp>
 
+#include <pthread.h>
+#include <sched.h>
+
 #include <chrono>
 #include <cstdint>
 #include <cstring>
@@ -136,9 +139,10 @@ int tdt_ref_decode_h(void *h, const uint8_t *blob, size_t len, uint8_t *out, siz
 // is not thread-safe, tdt_compression.hpp:349-360), messages statically interleaved.
 // Each worker encodes then decodes every one of its messages `reps` times and checks
 // the round trip.  Returns wall seconds (negative on a round-trip mismatch).
-double tdt_ref_bench(const uint8_t *data, const uint64_t *off, uint32_t n_msgs,
-                     float sample_fraction, int word_size, int threads, int reps,
-                     uint64_t *encoded_bytes_out) {
+// cpus (optional, `threads` entries): worker t is pinned to CPU cpus[t] before it starts.
+double tdt_ref_bench_pinned(const uint8_t *data, const uint64_t *off, uint32_t n_msgs,
+                            float sample_fraction, int word_size, int threads, int reps,
+                            uint64_t *encoded_bytes_out, const int *cpus) {
     if (threads < 1) threads = 1;
     std::vector<std::thread> pool;
     std::vector<uint64_t> enc_bytes(threads, 0);
@@ -146,6 +150,12 @@ double tdt_ref_bench(const uint8_t *data, const uint64_t *off, uint32_t n_msgs,
     auto t0 = std::chrono::steady_clock::now();
     for (int t = 0; t < threads; ++t) {
         pool.emplace_back([&, t]() {
+            if (cpus) {
+                cpu_set_t cs;
+                CPU_ZERO(&cs);
+                CPU_SET(cpus[t], &cs);
+                pthread_setaffinity_np(pthread_self(), sizeof(cs), &cs);
+            }
             TDTCompressionProtocol p(make_cfg(sample_fraction, word_size, 1024));
             p.update_network_metrics(10.0, 1.0);
             for (int r = 0; r < reps; ++r) {
@@ -170,6 +180,13 @@ double tdt_ref_bench(const uint8_t *data, const uint64_t *off, uint32_t n_msgs,
     }
     if (encoded_bytes_out) *encoded_bytes_out = tot;
     return anybad ? -s : s;
+}
+
+double tdt_ref_bench(const uint8_t *data, const uint64_t *off, uint32_t n_msgs,
+                     float sample_fraction, int word_size, int threads, int reps,
+                     uint64_t *encoded_bytes_out) {
+    return tdt_ref_bench_pinned(data, off, n_msgs, sample_fraction, word_size, threads, reps,
+                                encoded_bytes_out, nullptr);
 }
 
 } // extern "C"

@@ -108,6 +108,9 @@ struct PlanWS {
     uint8_t *dlarge = nullptr;  // decode: DMeta | block entries | block sums | tile entries | tile blocks
     uint32_t d_lcap = 0, d_bcap = 0, d_tcap = 0;
     CountHist eh, dh;  // encode / decode plan counts
+    // buffers replaced by a larger one: a graph captured on the context before the growth may
+    // still point at them, so they are freed only with the workspace
+    std::vector<void *> retired;
     // the large-message pipeline runs on `side` beside the medium/small lists (fork/join events)
     hipStream_t side = nullptr;
     hipEvent_t fork = nullptr, join = nullptr;
@@ -120,6 +123,8 @@ struct PlanWS {
         if (buf) (void)hipFree(buf);
         if (elarge) (void)hipFree(elarge);
         if (dlarge) (void)hipFree(dlarge);
+        for (void *p : retired) (void)hipFree(p);
+        retired.clear();
         buf = elarge = dlarge = nullptr;
         e_lcap = e_tcap = d_lcap = d_bcap = d_tcap = 0;
         eh.release();
@@ -138,6 +143,9 @@ struct tdt_ctx {
     std::mutex mu;
     // workspace: [0..64) counters (ticket, timeout), then one u64 look-back word per message
     uint8_t *ws = nullptr;
+    // device buffers a captured graph may still reference after a growth (ws, slot_sums): freed
+    // at tdt_ctx_destroy, never while the context lives
+    std::vector<void *> retired;
     size_t ws_bytes = 0;
     // per-chunk sums of tdt_decode_slots' two-pass scan (one u64 per 8192 messages; stream-ordered
     // like `ws`: one slotted decode per context at a time)
@@ -199,7 +207,7 @@ int ensure_ws(tdt_ctx *c, uint32_t n_msgs, hipStream_t s) {
     const size_t need = kCounterBytes + 8ull * (n_msgs + 1);
     if (need > c->ws_bytes) {
         if (int st = no_growth_in_capture(s)) return st;
-        if (c->ws) HIPCHK(hipFree(c->ws));
+        if (c->ws) c->retired.push_back(c->ws);  // (a graph captured earlier may use it)
         c->ws = nullptr;
         size_t cap = std::max<size_t>(need, c->ws_bytes * 2);
         HIPCHK(hipMalloc(&c->ws, cap));
@@ -335,7 +343,7 @@ int ensure_plan(PlanWS &w, uint32_t n, hipStream_t s) {
     const size_t need = 256 + 20ull * n;  // counters | small | medium | mid-sized | big | copy lists
     if (need > w.bytes) {
         if (int st = no_growth_in_capture(s)) return st;
-        if (w.buf) HIPCHK(hipFree(w.buf));
+        if (w.buf) w.retired.push_back(w.buf);  // (a graph captured earlier may use it)
         w.buf = nullptr;
         const size_t cap = std::max(need, w.bytes * 2);
         HIPCHK(hipMalloc(&w.buf, cap));
@@ -383,13 +391,6 @@ int join_side(PlanWS &w, hipStream_t s) {
     HIPCHK(hipStreamWaitEvent(s, w.join, 0));
     return TDT_OK;
 }
-// before a workspace is freed: the work of earlier calls that may still use it has finished
-// (only when a budget grows)
-int drain(PlanWS &w, hipStream_t s) {
-    HIPCHK(hipStreamSynchronize(s));
-    if (w.side) HIPCHK(hipStreamSynchronize(w.side));
-    return TDT_OK;
-}
 
 // Large-message budget: allocated on the first batch that may hold large messages, grown to
 // what an earlier plan claimed.
@@ -402,9 +403,9 @@ int ensure_elarge(PlanWS &w, int ws, hipStream_t s) {
     }
     if (w.elarge && lc == w.e_lcap && tc == w.e_tcap) return TDT_OK;
     if (w.elarge) {
-        int st = drain(w, s);
-        if (st) return st;
-        HIPCHK(hipFree(w.elarge));
+        // retired, not freed: earlier calls still queued, or a graph captured on the warm
+        // context, may use the old records (their launches carry the old budgets)
+        w.retired.push_back(w.elarge);
         w.elarge = nullptr;
         w.e_lcap = w.e_tcap = 0;
     }
@@ -718,7 +719,7 @@ size_t dlarge_bytes(uint32_t lcap, uint32_t bcap, uint32_t tcap) {
     return (size_t)lcap * sizeof(psy::DMeta) + 8ull * bcap + 4ull * tcap + 8ull * tcap;
 }
 
-int ensure_dlarge(PlanWS &w, hipStream_t s) {
+int ensure_dlarge(PlanWS &w) {
     uint32_t lc = w.d_lcap ? w.d_lcap : kDL0, bc = w.d_bcap ? w.d_bcap : kDB0, tc = w.d_tcap ? w.d_tcap : kDT0;
     if (w.dh.valid) {
         lc = std::max(lc, pow2_at_least(w.dh.v[2], kDL0, kDLmax));
@@ -727,9 +728,7 @@ int ensure_dlarge(PlanWS &w, hipStream_t s) {
     }
     if (w.dlarge && lc == w.d_lcap && bc == w.d_bcap && tc == w.d_tcap) return TDT_OK;
     if (w.dlarge) {
-        int st = drain(w, s);
-        if (st) return st;
-        HIPCHK(hipFree(w.dlarge));
+        w.retired.push_back(w.dlarge);  // (as ensure_elarge)
         w.dlarge = nullptr;
         w.d_lcap = w.d_bcap = w.d_tcap = 0;
     }
@@ -751,7 +750,7 @@ int launch_decode_slotted(tdt_ctx *c, PlanWS &pw, psy::DecodeArgs a, hipStream_t
     const bool copy_on = !H.valid || H.v[14] > 0;   // counter 7: UNCP blobs
     bool large_on = !H.valid || H.v[2] > 0;
     if (large_on && !capturing) {
-        st = ensure_dlarge(pw, s);
+        st = ensure_dlarge(pw);
         if (st) return st;
     }
     large_on = large_on && pw.dlarge;
@@ -1247,8 +1246,16 @@ int host_path(tdt_ctx *c, bool encode, const uint8_t *h_in, const uint64_t *h_in
     HIPCHK(hipSetDevice(c->device));
     std::lock_guard<std::mutex> lk(c->hmu);  // the pipeline slots belong to the context
     if (!c->pool) c->pool.reset(new CopyPool(c->copy_threads));
-    return encode ? host_encode(c, h_in, h_in_off, n_msgs, h_out, out_cap, h_out_off, h_status)
-                  : host_decode(c, h_in, h_in_off, n_msgs, h_out, out_cap, h_out_off, h_status);
+    const int st = encode ? host_encode(c, h_in, h_in_off, n_msgs, h_out, out_cap, h_out_off, h_status)
+                          : host_decode(c, h_in, h_in_off, n_msgs, h_out, out_cap, h_out_off, h_status);
+    if (st != TDT_OK) {
+        // an error mid-pipeline: the other slot's copies and kernels may still read the caller's
+        // input or write its output — drain both slots before the caller gets its buffers back
+        for (auto &h : c->hs)
+            if (h.stream) (void)hipStreamSynchronize(h.stream);
+        (void)hipGetLastError();
+    }
+    return st;
 }
 
 }  // namespace
@@ -1374,6 +1381,7 @@ void tdt_ctx_destroy(tdt_ctx *ctx) {
     if (ctx->slot_sums) (void)hipFree(ctx->slot_sums);
     if (ctx->cp_buf) (void)hipFree(ctx->cp_buf);
     if (ctx->cp_idx) (void)hipFree(ctx->cp_idx);
+    for (void *p : ctx->retired) (void)hipFree(p);
     ctx->pw.release();
     if (ctx->hbases) (void)hipFree(ctx->hbases);
     if (ctx->astream) (void)hipStreamSynchronize(ctx->astream);
@@ -1410,6 +1418,13 @@ void tdt_ctx_set_size_hint(tdt_ctx *ctx, uint64_t bytes) { ctx->size_hint.store(
 
 int tdt_ctx_set_option(tdt_ctx *ctx, int option, uint64_t value) {
     if (!ctx) return set_err(TDT_E_ARG, "null context");
+    if (option == TDT_OPT_COPY_THREADS) {
+        // the copy pool belongs to the host pipeline (hmu); lock order everywhere: hmu, then mu
+        std::lock_guard<std::mutex> hl(ctx->hmu);
+        ctx->copy_threads = (int)std::max<uint64_t>(1, std::min<uint64_t>(value, 64));
+        ctx->pool.reset();
+        return TDT_OK;
+    }
     std::lock_guard<std::mutex> lk(ctx->mu);
     switch (option) {
         case TDT_OPT_LARGE_MIN: ctx->large_min = value; return TDT_OK;
@@ -1417,12 +1432,6 @@ int tdt_ctx_set_option(tdt_ctx *ctx, int option, uint64_t value) {
         case TDT_OPT_NO_SIDE_STREAM: ctx->no_side = value != 0; return TDT_OK;
         case TDT_OPT_SMALL_ON_CALLER_STREAM: ctx->small_main = value != 0; return TDT_OK;
         case TDT_OPT_NO_TWO_PHASE: ctx->no_two_phase = value != 0; return TDT_OK;
-        case TDT_OPT_COPY_THREADS: {
-            std::lock_guard<std::mutex> hl(ctx->hmu);
-            ctx->copy_threads = (int)std::max<uint64_t>(1, std::min<uint64_t>(value, 64));
-            ctx->pool.reset();
-            return TDT_OK;
-        }
     }
     return set_err(TDT_E_ARG, "unknown option");
 }
@@ -1636,17 +1645,16 @@ int tdt_analyze_host(tdt_ctx *ctx, const uint8_t *h_in, const uint64_t *h_in_off
     const size_t o_map = align_up(o_ent + 8ull * n_msgs * ws, 256);
     const size_t o_st = align_up(o_map + 4ull * n_msgs * ws, 256);
     const size_t total = align_up(o_st + 4ull * n_msgs, 256);
-    int st;
-    {
-        std::lock_guard<std::mutex> lk(ctx->mu);
-        st = ensure_host_dev(ctx, total);
-    }
+    // h_dev and astream belong to the host paths (hmu, held for the whole call, so a second
+    // caller cannot reallocate h_dev under this one); encode_common then takes mu: the lock
+    // order everywhere is hmu, then mu
+    std::lock_guard<std::mutex> hl(ctx->hmu);
+    int st = ensure_host_dev(ctx, total);
     if (st) return st;
     uint8_t *d = ctx->h_dev;
     std::vector<uint64_t> tmp(n_msgs + 1);
     for (uint32_t i = 0; i <= n_msgs; ++i) tmp[i] = h_in_off[i] - h_in_off[0];
     // on the context's own stream (synchronising that stream only, not the device)
-    std::lock_guard<std::mutex> hl(ctx->hmu);
     if (!ctx->astream) HIPCHK(hipStreamCreateWithFlags(&ctx->astream, hipStreamNonBlocking));
     hipStream_t s = ctx->astream;
     HIPCHK(hipMemcpyAsync(d, h_in + h_in_off[0], in_bytes, hipMemcpyHostToDevice, s));
@@ -1701,7 +1709,7 @@ static int scan_sizes(tdt_ctx *ctx, uint64_t *d_slot_off, uint32_t n_msgs, hipSt
         std::lock_guard<std::mutex> lk(ctx->mu);
         if (nb > ctx->slot_sums_n) {
             if (int st = no_growth_in_capture(stream)) return st;
-            if (ctx->slot_sums) HIPCHK(hipFree(ctx->slot_sums));
+            if (ctx->slot_sums) ctx->retired.push_back(ctx->slot_sums);  // (a captured graph may use it)
             ctx->slot_sums = nullptr;
             HIPCHK(hipMalloc(&ctx->slot_sums, 8ull * nb));
             ctx->slot_sums_n = nb;

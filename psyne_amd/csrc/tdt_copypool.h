@@ -67,12 +67,14 @@ class CopyPool {
     CopyPool(const CopyPool &) = delete;
     CopyPool &operator=(const CopyPool &) = delete;
 
-    // dst[0, bytes) = src[0, bytes); returns when every part is copied
+    // dst[0, bytes) = src[0, bytes); returns when every part is copied.  Thread-safe: the pool
+    // runs one job at a time (job_ is shared), so concurrent callers take turns.
     void copy(void *dst, const void *src, size_t bytes) {
         if (bytes < kParMin || th_.empty()) {
             std::memcpy(dst, src, bytes);
             return;
         }
+        std::lock_guard<std::mutex> one(call_);
         auto job = std::make_shared<Job>();
         job->d = static_cast<uint8_t *>(dst);
         job->s = static_cast<const uint8_t *>(src);
@@ -130,6 +132,7 @@ class CopyPool {
     }
 
     std::vector<std::thread> th_;
+    std::mutex call_;  // one copy() at a time
     std::mutex m_;
     std::condition_variable cv_, done_;
     bool stop_ = false;

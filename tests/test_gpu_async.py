@@ -175,3 +175,41 @@ def test_batches_of_other_shapes_on_a_warm_context():
         assert torch.equal(s.dec[: data.numel()], data), k
         assert int(s.est.abs().sum()) == 0 and int(s.dst.abs().sum()) == 0
     assert codec.error_flags() == 0
+
+
+def test_graph_replay_after_workspace_growth():
+    """A graph captured on a warm context keeps working after a later eager batch has grown the
+    context's workspaces (more large messages than the large-message budget held): grown
+    workspaces retire the old buffers instead of freeing them (tdt_api.hip
+    ensure_elarge / ensure_dlarge / ensure_plan)."""
+    data_h, off_h = _mixed(34)
+    data = torch.from_numpy(data_h).cuda()
+    off = torch.from_numpy(off_h).cuda()
+    codec = _codec()
+    s = _Slotted(codec, data, off)
+    s.run()
+    torch.cuda.synchronize()
+    eager = s.blobs()
+    gr = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(gr):
+        s.run()
+    # a batch with 1,100 messages of 300 KiB (the starting budget holds 1,024 large messages),
+    # twice: the second call grows the large-message and plan workspaces from the first's counts
+    rng = np.random.default_rng(35)
+    big = [_gradient(rng, 300 * 1024) for _ in range(1100)]
+    boff = np.zeros(len(big) + 1, np.int64)
+    boff[1:] = np.cumsum([m.size for m in big])
+    bdata = torch.from_numpy(np.concatenate(big)).cuda()
+    b = _Slotted(codec, bdata, torch.from_numpy(boff).cuda())
+    for _ in range(2):
+        b.run()
+        torch.cuda.synchronize()
+        assert torch.equal(b.dec, bdata) and int(b.est.abs().sum()) == 0 and int(b.dst.abs().sum()) == 0
+    s.zero()
+    torch.cuda.synchronize()
+    gr.replay()
+    torch.cuda.synchronize()
+    assert s.blobs() == eager
+    assert torch.equal(s.dec[: data.numel()], data)
+    assert int(s.est.abs().sum()) == 0 and int(s.dst.abs().sum()) == 0
+    assert codec.error_flags() == 0

@@ -144,6 +144,46 @@ def test_c4_full_batch_bitexact():
     assert torch.equal(back[:int(off[-1])], data)
 
 
+@pytest.mark.timeout(900)
+def test_c5_per_rank_batch_bitexact():
+    """BASELINE configs[4] (C5) at ONE rank's size, as bench.py --workload c5 generates it: 524,288 x
+    64 KiB (32 GiB) gradient-like messages per GPU (seed 0x5EED0005 + rank 0).  Input offsets run to
+    32 GiB and slot offsets past 64 GiB, where offset-width bugs live (round 3 found one past 2 GiB).
+    The whole batch is encoded slotted and decoded back on the device; the blobs of the first and
+    last 8,192 messages and of 8,192 random ones in between are compared byte for byte with the
+    oracle's."""
+    import bench
+    n, mb = 524288, 65536
+    data = bench.gen_gradient(torch, n, mb, 0x5EED0005, torch.device("cuda"))
+    off = torch.arange(n + 1, dtype=torch.int64, device="cuda") * mb
+    codec = make_codec()
+    out, slots, lens, st = codec.encode_into(data, off)
+    torch.cuda.synchronize()
+    assert int(st[:n].abs().sum()) == 0
+    sl = slots.cpu().numpy().astype(np.int64)
+    ln = lens[:n].cpu().numpy().astype(np.int64)
+    assert sl[n - 1] > (64 << 30) and int(sl[n]) <= out.numel()
+    orc = Oracle()
+    rng = np.random.default_rng(0xC5)
+    mid = np.sort(rng.choice(np.arange(8192, n - 8192), 8192, replace=False))
+    for idx in (np.arange(8192), np.arange(n - 8192, n), mid):
+        ti = torch.from_numpy(idx).cuda()
+        host = data.view(n, mb).index_select(0, ti).cpu().numpy().reshape(-1)
+        want, wslot, wlen = orc.encode_slotted(host, np.arange(idx.size + 1, dtype=np.uint64) * mb, bandwidth=10.0)
+        assert np.array_equal(ln[idx], wlen.astype(np.int64)), "blob lengths differ"
+        # the GPU blobs of these messages, gathered on the device into one buffer
+        got = torch.cat([out[int(sl[i]):int(sl[i]) + int(ln[i])] for i in idx]).cpu().numpy()
+        g = 0
+        for k, i in enumerate(idx):
+            L, w = int(ln[i]), int(wslot[k])
+            assert np.array_equal(got[g:g + L], want[w:w + L]), "blob %d differs" % i
+            g += L
+    back, dsl, dln, dst = codec.decode_into(out, slots, in_lengths=lens)
+    torch.cuda.synchronize()
+    assert int(dst[:n].abs().sum()) == 0
+    assert torch.equal(back[:n * mb], data)
+
+
 @pytest.mark.timeout(600)
 def test_c4_zipf_full_range_bitexact():
     """C4's size distribution over its FULL range (bench.zipf_sizes: 64 B - 1 MiB, Zipf(1.5),

@@ -104,3 +104,31 @@ def test_bench_refuses_world_size_mismatch():
     p = subprocess.run([sys.executable, "bench.py", "--gpus", "2"], cwd=root, env=env, capture_output=True,
                        text=True, timeout=120)
     assert p.returncode == 2 and "WORLD_SIZE=3" in p.stderr
+
+
+def test_bench_launcher_never_initialises_hip():
+    """`bench.py --gpus N` (the driver's SCALE launch) starts its ranks from a parent that never
+    touches HIP: it counts GPUs from the KFD topology, never imports torch, and refuses more GPUs
+    than the host has with exit code 2 and a clear message."""
+    import subprocess
+    import sys
+    root = pathlib.Path(__file__).resolve().parents[1]
+    env = {k: v for k, v in os.environ.items() if k != "PSYNE_BENCH_SHARED_DEVICE"}
+    env.pop("WORLD_SIZE", None)
+    p = subprocess.run([sys.executable, str(root / "bench.py"), "--gpus", "9999"], capture_output=True, text=True,
+                       timeout=120, env=env, cwd=str(root))
+    assert p.returncode == 2, p.stdout + p.stderr
+    assert "--gpus 9999 but only" in p.stderr and "visible GPU" in p.stderr
+    probe = ("import sys; sys.argv = ['bench.py', '--gpus', '9999']; import bench; "
+             "rc = bench.launch_ranks(bench.parse()); maps = open('/proc/self/maps').read(); "
+             "print(rc, 'libamdhip64' in maps, 'torch' in sys.modules, 'psyne_amd' in sys.modules)")
+    p = subprocess.run([sys.executable, "-c", probe], capture_output=True, text=True, timeout=120, env=env,
+                       cwd=str(root))
+    assert p.stdout.split() == ["2", "False", "False", "False"], p.stdout + p.stderr
+
+
+def test_visible_gpus_and_cpulist_parsing(tmp_path, monkeypatch):
+    import bench
+    assert bench.parse_cpulist("0-3,8,10-11\n") == {0, 1, 2, 3, 8, 10, 11}
+    monkeypatch.setenv("ROCR_VISIBLE_DEVICES", "-1")
+    assert bench.visible_gpus() == []

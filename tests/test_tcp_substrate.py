@@ -74,6 +74,20 @@ def test_tdt_substrate_gpu_loopback(tmp_path):
 
 
 @pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_tdt_substrate_gpu_loopback_c1_workload(tmp_path):
+    """BASELINE configs[0] at its own workload (tcp_tdt_benchmark.cpp:542-543): 1,000 tensors of
+    256 Ki float32 (1 MiB) GRADIENTS over loopback TCP through TdtSubstrate on both ends; the
+    receiver verifies every payload and every one of the 1,000 wire frames equals the oracle's
+    encoding of its tensor."""
+    r = run("--codec", "gpu", "--count", "1000", "--floats", str(256 * 1024), "--batch", "50", "--port", "18184",
+            "--dump", str(tmp_path), timeout=300)
+    assert r["mismatches"] == 0 and r["tensors"] == 1000
+    assert r["compression_ratio"] > 1.2
+    check_frames_vs_oracle(tmp_path, 1000, 256 * 1024)
+
+
+@pytest.mark.gpu
 def test_tdt_substrate_decorator_cpp():
     # crafted frame claiming 0xFFFFFFF0 decoded bytes rejected before decoding; the connection
     # stays usable; one oversized frame in a batch gets TDT_E_CAPACITY, its neighbours decode
