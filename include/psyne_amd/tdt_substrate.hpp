@@ -23,8 +23,9 @@
 //     Base: the vtable to implement — psyne::behaviors::SubstrateBehavior in a psyne build
 //     (every method here matches its signature, so it overrides), an empty struct otherwise.
 //     send_batch / receive_batch move many messages per GPU call through the C ABI host
-//     pipeline (tdt_encode_host / tdt_decode_host: chunked, H2D / kernel / D2H overlapped on two
-//     streams), which is how the codec reaches PCIe rates instead of per-message latency.
+//     pipeline (tdt_encode_host_v / tdt_decode_host: chunked, H2D / kernel / D2H overlapped on
+//     two streams) with a sender and a receiver thread overlapping the socket with the codec,
+//     which is how the codec reaches the link's rate instead of per-message latency.
 #pragma once
 
 #include <arpa/inet.h>
@@ -36,11 +37,15 @@
 
 #include <psyne_amd/hip_tdt_protocol.hpp>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <exception>
+#include <memory>
 #include <mutex>
 #include <new>
 #include <stdexcept>
@@ -107,7 +112,7 @@ public:
     // TRANSPORT (:68-91): u32 length, then the bytes
     void transport_send(void *data, size_t size) {
         if (!is_connected()) throw std::runtime_error("TCP: Not connected");
-        std::lock_guard<std::mutex> lk(mu_);
+        std::lock_guard<std::mutex> lk(smu_);
         const uint32_t hdr = static_cast<uint32_t>(size);
         if (!write_all(&hdr, sizeof(hdr)) || !write_all(data, size)) {
             connected_.store(false);
@@ -120,7 +125,7 @@ public:
     // (:96-150) one frame into buffer (the caller learns no length: SubstrateBehavior's shape)
     void transport_receive(void *buffer, size_t buffer_size) {
         if (!is_connected()) throw std::runtime_error("TCP: Not connected");
-        std::lock_guard<std::mutex> lk(mu_);
+        std::lock_guard<std::mutex> lk(rmu_);
         uint32_t hdr = 0;
         if (!read_all(&hdr, sizeof(hdr))) fail("TCP receive failed: connection lost");
         if (hdr == 0) throw std::runtime_error("TCP receive failed: TCP: Received empty message");
@@ -143,7 +148,7 @@ public:
     // and returns false)
     bool try_transport_receive(void *buffer, size_t buffer_size, size_t &received_size) {
         if (!is_connected()) return false;
-        std::lock_guard<std::mutex> lk(mu_);
+        std::lock_guard<std::mutex> lk(rmu_);
         uint32_t hdr = 0;
         const ssize_t got = ::recv(fd_, &hdr, sizeof(hdr), MSG_PEEK | MSG_DONTWAIT);
         if (got < (ssize_t)sizeof(hdr)) return false;
@@ -176,6 +181,8 @@ public:
     size_t get_packets_sent() const { return packets_sent_; }
     size_t get_packets_received() const { return packets_received_; }
     const std::string &get_host() const { return host_; }
+    // shut the connection down (unblocks a thread inside a send or receive); the destructor joins
+    void close() { close_socket(); }
     uint16_t get_port() const { return port_; }
     bool is_server_mode() const { return is_server_; }
 
@@ -241,7 +248,7 @@ private:
     int fd_ = -1, listen_fd_ = -1;
     std::thread accept_thread_, connect_thread_;
     std::atomic<bool> connected_{false}, stop_{false};
-    std::mutex mu_;
+    std::mutex smu_, rmu_;  // one sender and one receiver at a time (the two directions are independent)
     size_t slab_size_ = 0;
     size_t bytes_sent_ = 0, bytes_received_ = 0, packets_sent_ = 0, packets_received_ = 0;
 };
@@ -259,9 +266,48 @@ inline int64_t tdt_claimed_size(const uint8_t *blob, size_t len) {
     return (int64_t)orig;
 }
 
+
 struct NoSubstrateBase {};
 
+// Pinned (page-locked) host buffer from the codec library (tdt_host_alloc): the host pipeline
+// DMAs it directly (no staging copy).
+class PinnedBuffer {
+public:
+    PinnedBuffer() = default;
+    ~PinnedBuffer() { tdt_host_free(p_); }
+    PinnedBuffer(const PinnedBuffer &) = delete;
+    PinnedBuffer &operator=(const PinnedBuffer &) = delete;
+    void reserve(size_t bytes) {
+        if (bytes <= cap_) return;
+        tdt_host_free(p_);
+        p_ = nullptr;
+        cap_ = 0;
+        void *q = nullptr;
+        if (tdt_host_alloc(bytes, &q) != TDT_OK) throw std::bad_alloc();
+        p_ = static_cast<uint8_t *>(q);
+        cap_ = bytes;
+    }
+    uint8_t *data() { return p_; }
+    size_t capacity() const { return cap_; }
+
+private:
+    uint8_t *p_ = nullptr;
+    size_t cap_ = 0;
+};
+
 // Decorator: TDT payload compression on the GPU between the channel and a framed substrate.
+//
+// Batches are pipelined (docs/tdt_attribution.md:62-75's intent; tcp_simple.hpp:68-91 framing):
+//  * send_batch encodes its messages in sub-batches (tdt_encode_host_v: the caller's buffers are
+//    gathered straight into pinned staging, no packing copy) into a ring of pinned output
+//    buffers; a sender thread writes each finished sub-batch's frames to Inner while the next
+//    sub-batch is on the GPU.  It returns once its messages are encoded (the caller may reuse
+//    them); frames leave in order; flush() waits until every queued frame is on the wire.
+//  * receiving runs as three stages once receive_batch has started them: a receiver thread reads
+//    frames from Inner into a ring of pinned buffers (sealing one when it is full or the socket
+//    has nothing more for now), a decoder thread decodes each sealed buffer on the GPU (direct
+//    H2D from the pinned frames, D2H into a pinned payload buffer), and receive_batch hands the
+//    decoded payloads to the caller (parallel copy) — socket, GPU and the caller's copy overlap.
 template <class Inner, class Base = NoSubstrateBase>
 class TdtSubstrate : public Base {
 public:
@@ -287,6 +333,28 @@ public:
         codec_.update_network_metrics(defaults().bandwidth_mbps, defaults().latency_ms);
         name_ = std::string("TDT+") + inner_.substrate_name();
     }
+    ~TdtSubstrate() {
+        try {
+            if (tx_thread_.joinable()) flush();
+        } catch (...) {
+        }
+        {
+            std::lock_guard<std::mutex> lk(tx_mu_);
+            tx_stop_ = true;
+        }
+        tx_cv_.notify_all();
+        {
+            std::lock_guard<std::mutex> lk(rx_mu_);
+            rx_stop_ = true;
+        }
+        rx_cv_.notify_all();
+        if constexpr (requires(Inner &s) { s.close(); }) {
+            if (rx_thread_.joinable()) inner_.close();  // (the receiver may sit inside a read)
+        }
+        if (tx_thread_.joinable()) tx_thread_.join();
+        if (rx_thread_.joinable()) rx_thread_.join();
+        if (dec_thread_.joinable()) dec_thread_.join();
+    }
     TdtSubstrate(const TdtSubstrate &) = delete;
     TdtSubstrate &operator=(const TdtSubstrate &) = delete;
 
@@ -298,8 +366,9 @@ public:
     void deallocate_memory_slab(void *p) { inner_.deallocate_memory_slab(p); }
 
     // TRANSPORT: one message = one frame (UNCP when the policy is off, exactly as
-    // TDTCompressionProtocol::encode :227-266)
+    // TDTCompressionProtocol::encode :227-266); after any queued batch frames
     void transport_send(void *data, size_t size) {
+        if (tx_thread_.joinable()) flush();
         std::vector<uint8_t> blob = codec_.encode(data, size);
         inner_.transport_send(blob.data(), blob.size());
         raw_sent_ += size;
@@ -314,7 +383,7 @@ public:
         auto pause = std::chrono::microseconds(1);
         while (!try_transport_receive(buffer, buffer_size, got)) {
             if constexpr (requires(Inner &s) { s.is_connected(); }) {
-                if (!inner_.is_connected()) throw std::runtime_error("TCP: Not connected");
+                if (!inner_.is_connected() && !frames_ready()) throw std::runtime_error("TCP: Not connected");
             }
             std::this_thread::sleep_for(pause);
             if (pause < std::chrono::microseconds(200)) pause *= 2;
@@ -322,8 +391,35 @@ public:
     }
 
     // (tcp_simple.hpp:153-194 shape) false when no frame is waiting; otherwise one frame is
-    // taken from Inner, checked, decoded into buffer, and its decoded size returned.
+    // taken (from Inner, or from the receive pipeline once receive_batch started it), checked,
+    // decoded into buffer, and its decoded size returned.
     bool try_transport_receive(void *buffer, size_t buffer_size, size_t &received_size) {
+        if (rx_thread_.joinable()) {
+            release_views();
+            std::unique_lock<std::mutex> lk(rx_mu_);
+            if (rx_err_ && !rx_front_decoded()) std::rethrow_exception(rx_err_);
+            RxBuf *b = rx_front_decoded();
+            if (!b) return false;
+            const size_t k = b->used;
+            rx_consume(1);  // (the frame's payload stays put until its buffer is refilled: see rx_consume)
+            const int64_t claimed = b->claim[k];
+            const int32_t st = b->st[k];
+            const uint64_t n = b->doff[k + 1] - b->doff[k];
+            if (claimed > (int64_t)buffer_size) {
+                rx_release_if_done(b);
+                lk.unlock();
+                rx_cv_.notify_all();
+                throw std::runtime_error("TDT: decoded message larger than the buffer");
+            }
+            if (st == TDT_OK && n) std::memcpy(buffer, b->dec.data() + b->doff[k], n);
+            rx_release_if_done(b);
+            lk.unlock();
+            rx_cv_.notify_all();
+            if (st != TDT_OK) throw std::runtime_error(tdt_status_string(st));
+            received_size = n;
+            last_received_ = n;
+            return true;
+        }
         stage_.resize(frame_capacity(buffer_size));
         size_t flen = 0;
         if (!inner_.try_transport_receive(stage_.data(), stage_.size(), flen)) return false;
@@ -351,91 +447,565 @@ public:
     size_t last_received_size() const { return last_received_; }
     // wire bytes / payload bytes sent so far
     double wire_ratio() const { return raw_sent_ ? double(wire_sent_) / double(raw_sent_) : 1.0; }
+    // keep a copy of each send_batch's blobs for last_batch() (tests; off by default)
+    void record_last_batch(bool on) { record_last_ = on; }
 
-    // Many messages per GPU call: pack → tdt_encode_host (one pipelined batch) → one frame per
-    // blob, in order.  Returns the wire bytes.
+    // Many messages per GPU call: the batch is encoded in sub-batches and queued for the sender
+    // thread (one frame per blob, in order).  Returns the wire bytes of this batch.
     size_t send_batch(const void *const *data, const size_t *sizes, size_t n) {
+        static_assert(sizeof(size_t) == sizeof(uint64_t), "size_t is 64-bit");
         if (n == 0) return 0;
-        std::vector<uint64_t> off(n + 1, 0);
-        for (size_t i = 0; i < n; ++i) off[i + 1] = off[i] + sizes[i];
-        pack_.resize(off[n]);
-        for (size_t i = 0; i < n; ++i) std::memcpy(pack_.data() + off[i], data[i], sizes[i]);
-        uint64_t cap = 0;
-        for (size_t i = 0; i < n; ++i) cap += tdt_encode_bound(sizes[i], codec_.word_size());
-        enc_.resize(cap);
-        std::vector<uint64_t> &eoff = eoff_;
-        eoff.assign(n + 1, 0);
-        std::vector<int32_t> st(n);
-        if (tdt_encode_host(codec_.context(), pack_.data(), off.data(), (uint32_t)n, enc_.data(), cap, eoff.data(),
-                            st.data()) != TDT_OK)
-            throw std::runtime_error(std::string("TDT: GPU batch encode failed: ") + tdt_last_error());
-        for (size_t i = 0; i < n; ++i) {
-            if (st[i] != TDT_OK) throw std::runtime_error(tdt_status_string(st[i]));
-            inner_.transport_send(enc_.data() + eoff[i], eoff[i + 1] - eoff[i]);
+        rethrow_tx();
+        if (!tx_thread_.joinable()) tx_thread_ = std::thread([this] { tx_loop(); });
+        const auto *msgs = reinterpret_cast<const uint8_t *const *>(data);
+        const auto *sz = reinterpret_cast<const uint64_t *>(sizes);
+        if (record_last_) {
+            enc_.clear();
+            eoff_.assign(1, 0);
         }
-        raw_sent_ += off[n];
-        wire_sent_ += eoff[n];
-        return eoff[n];
+        size_t wire = 0;
+        for (size_t i = 0; i < n;) {
+            size_t m = 0;
+            uint64_t payload = 0, cap = 0;
+            while (i + m < n && (m == 0 || (payload + sz[i + m] <= kSubBytes && m < kSubFrames))) {
+                payload += sz[i + m];
+                cap += tdt_encode_bound(sz[i + m], codec_.word_size());
+                ++m;
+            }
+            TxBuf &b = tx_acquire();
+            b.mem.reserve(cap);
+            b.off.assign(m + 1, 0);
+            b.st.assign(m, 0);
+            if (tdt_encode_host_v(codec_.context(), msgs + i, sz + i, (uint32_t)m, b.mem.data(), cap, b.off.data(),
+                                  b.st.data()) != TDT_OK) {
+                tx_release_unused(b);
+                throw std::runtime_error(std::string("TDT: GPU batch encode failed: ") + tdt_last_error());
+            }
+            for (size_t k = 0; k < m; ++k)
+                if (b.st[k] != TDT_OK) {
+                    tx_release_unused(b);
+                    throw std::runtime_error(tdt_status_string(b.st[k]));
+                }
+            b.n = m;
+            if (record_last_) {
+                const uint64_t base = enc_.size();
+                enc_.insert(enc_.end(), b.mem.data(), b.mem.data() + b.off[m]);
+                for (size_t k = 1; k <= m; ++k) eoff_.push_back(base + b.off[k]);
+            }
+            raw_sent_ += payload;
+            wire_sent_ += b.off[m];
+            wire += b.off[m];
+            tx_submit(b);
+            i += m;
+        }
+        return wire;
     }
 
-    // The blobs of the last send_batch (frame i = last_batch()[offsets[i] .. offsets[i+1])).
+    // Every frame queued by send_batch is on the wire (rethrows a send error).
+    void flush() {
+        std::unique_lock<std::mutex> lk(tx_mu_);
+        tx_cv_.wait(lk, [&] { return tx_queue_.empty() && !tx_busy_; });
+        lk.unlock();
+        rethrow_tx();
+    }
+
+    // The blobs of the last send_batch when record_last_batch(true) (frame i =
+    // last_batch()[offsets[i] .. offsets[i+1])).
     const std::vector<uint8_t> &last_batch() const { return enc_; }
     const std::vector<uint64_t> &last_batch_offsets() const { return eoff_; }
 
-    // Receive n frames (each expected to decode to <= max_msg bytes) and decode them in one GPU
-    // call; out / out_off (n+1) receive the payloads back to back.  Returns the per-message
-    // status: a frame whose header claims more than max_msg is not decoded (TDT_E_CAPACITY,
-    // empty payload) and does not affect the others; decode errors keep their own status.
+    // Receive n frames (each expected to decode to <= max_msg bytes) and decode them; out /
+    // out_off (n+1) receive the payloads back to back.  Returns the per-message status: a frame
+    // whose header claims more than max_msg is not decoded (TDT_E_CAPACITY, empty payload) and
+    // does not affect the others; decode errors keep their own status.
     std::vector<int32_t> receive_batch(size_t n, size_t max_msg, std::vector<uint8_t> &out,
                                        std::vector<uint64_t> &out_off) {
-        const size_t fcap = frame_capacity(max_msg);
-        std::vector<uint64_t> boff(n + 1, 0);
+        release_views();
         std::vector<int32_t> st(n, TDT_OK);
-        std::vector<bool> rejected(n, false);
-        pack_.resize(n * fcap + 4);
-        uint64_t decoded = 0;
-        for (size_t i = 0; i < n; ++i) {
-            size_t flen = 0;
-            auto pause = std::chrono::microseconds(1);
-            while (!inner_.try_transport_receive(pack_.data() + boff[i], fcap, flen)) {
-                if constexpr (requires(Inner &s) { s.is_connected(); }) {
-                    if (!inner_.is_connected()) throw std::runtime_error("TCP: Not connected");
-                }
-                std::this_thread::sleep_for(pause);
-                if (pause < std::chrono::microseconds(200)) pause *= 2;
-            }
-            const int64_t claimed = tdt_claimed_size(pack_.data() + boff[i], flen);
-            if (claimed > (int64_t)max_msg) {  // replace by an empty UNCP blob
-                static const uint8_t kEmpty[4] = {0x50, 0x43, 0x4E, 0x55};
-                std::memcpy(pack_.data() + boff[i], kEmpty, 4);
-                flen = 4;
-                rejected[i] = true;
-            } else if (claimed > 0) {
-                decoded += (uint64_t)claimed;
-            }
-            boff[i + 1] = boff[i] + flen;
-        }
-        out.resize(decoded ? decoded : 1);
         out_off.assign(n + 1, 0);
-        if (tdt_decode_host(codec_.context(), pack_.data(), boff.data(), (uint32_t)n, out.data(), decoded,
-                            out_off.data(), st.data()) != TDT_OK)
-            throw std::runtime_error(std::string("TDT: GPU batch decode failed: ") + tdt_last_error());
-        for (size_t i = 0; i < n; ++i)
-            if (rejected[i]) st[i] = TDT_E_CAPACITY;
-        out.resize(out_off[n]);
+        if (n == 0) return st;
+        start_rx(max_msg);
+        size_t done = 0;
+        uint64_t cur = 0;
+        while (done < n) {
+            RxBuf *b = wait_front();
+            // (only this thread consumes: the buffer's frames and payloads stay put until released)
+            const size_t k0 = b->used, k1 = std::min(b->n, k0 + (n - done));
+            uint64_t total = 0;
+            for (size_t k = k0; k < k1; ++k)
+                if (b->claim[k] <= (int64_t)max_msg) total += b->claim[k] > 0 ? (uint64_t)b->claim[k] : 0u;
+            if (out.size() < cur + total) out.resize(cur + total);
+            // payloads decoded ahead are contiguous in b->dec: runs of them leave in one parallel
+            // copy; a frame over this call's max_msg is not delivered; one the decoder skipped
+            // (over its limit at the time, within this call's) is decoded now
+            size_t run0 = k0;
+            auto copy_run = [&](size_t e) {
+                const uint64_t a0 = b->doff[run0], len = b->doff[e] - a0;
+                if (len && tdt_host_copy(codec_.context(), out.data() + cur, b->dec.data() + a0, len) != TDT_OK)
+                    throw std::runtime_error(std::string("TDT: host copy failed: ") + tdt_last_error());
+                for (size_t k = run0; k < e; ++k) out_off[done + (k - k0) + 1] = cur + (b->doff[k + 1] - a0);
+                cur += len;
+            };
+            for (size_t k = k0; k < k1; ++k) {
+                const size_t j = done + (k - k0);
+                const int64_t c = b->claim[k];
+                if (c <= (int64_t)max_msg && c <= (int64_t)b->lim) {
+                    st[j] = b->st[k];
+                    continue;
+                }
+                copy_run(k);
+                run0 = k + 1;
+                if (c > (int64_t)max_msg) {
+                    st[j] = TDT_E_CAPACITY;
+                } else {
+                    const uint64_t fo[2] = {b->off[k], b->off[k + 1]};
+                    uint64_t oo[2] = {0, 0};
+                    if (tdt_decode_host(codec_.context(), b->mem.data(), fo, 1, out.data() + cur, (uint64_t)c, oo,
+                                        &st[j]) != TDT_OK)
+                        throw std::runtime_error(std::string("TDT: GPU decode failed: ") + tdt_last_error());
+                    cur += oo[1];
+                }
+                out_off[j + 1] = cur;
+            }
+            copy_run(k1);
+            done += k1 - k0;
+            {
+                std::lock_guard<std::mutex> lk(rx_mu_);
+                rx_consume(k1 - k0);
+                rx_release_if_done(b);
+            }
+            rx_cv_.notify_all();
+        }
+        out.resize(cur);
         return st;
     }
 
+    // Zero-copy receive: views of the next n decoded payloads in the pipeline's pinned buffers,
+    // valid until the next receive call on this substrate (or release_views()).  Statuses as
+    // receive_batch.
+    struct FrameView {
+        const uint8_t *data;
+        uint64_t size;
+        int32_t status;
+    };
+    std::vector<FrameView> receive_batch_views(size_t n, size_t max_msg) {
+        release_views();
+        std::vector<FrameView> v(n, FrameView{nullptr, 0, TDT_OK});
+        if (n == 0) return v;
+        start_rx(max_msg);
+        size_t done = 0;
+        while (done < n) {
+            // a consumer holding too many buffers would starve the receiver: move the held
+            // payloads out (one copy) and give their buffers back
+            if (rx_held_.size() >= kRxMax / 2) migrate_views(v);
+            RxBuf *b = wait_front();
+            const size_t k0 = b->used, k1 = std::min(b->n, k0 + (n - done));
+            holds_.push_back(Hold{b, done, done + (k1 - k0), k0});
+            for (size_t k = k0; k < k1; ++k) {
+                FrameView &f = v[done + (k - k0)];
+                const int64_t c = b->claim[k];
+                if (c > (int64_t)max_msg) {
+                    f.status = TDT_E_CAPACITY;
+                } else if (c > (int64_t)b->lim) {  // skipped by the decoder: decoded now
+                    late_.emplace_back((size_t)std::max<int64_t>(c, 1));
+                    const uint64_t fo[2] = {b->off[k], b->off[k + 1]};
+                    uint64_t oo[2] = {0, 0};
+                    if (tdt_decode_host(codec_.context(), b->mem.data(), fo, 1, late_.back().data(), (uint64_t)c, oo,
+                                        &f.status) != TDT_OK)
+                        throw std::runtime_error(std::string("TDT: GPU decode failed: ") + tdt_last_error());
+                    f.data = late_.back().data();
+                    f.size = oo[1];
+                } else {
+                    f.data = b->dec.data() + b->doff[k];
+                    f.size = b->doff[k + 1] - b->doff[k];
+                    f.status = b->st[k];
+                }
+            }
+            done += k1 - k0;
+            {
+                std::lock_guard<std::mutex> lk(rx_mu_);
+                rx_consume(k1 - k0);
+                if (b->used == b->n) {  // consumed: held (not reused) while the views live
+                    rx_order_.erase(rx_order_.begin());
+                    rx_held_.push_back(b);
+                }
+            }
+            rx_cv_.notify_all();
+        }
+        return v;
+    }
+    // The views of the last receive_batch_views are no longer used: their buffers return to
+    // the pipeline.  (Every receive call does this first.)
+    void release_views() {
+        {
+            std::lock_guard<std::mutex> lk(rx_mu_);
+            for (RxBuf *b : rx_held_) b->free = true;
+            rx_held_.clear();
+        }
+        late_.clear();
+        holds_.clear();
+        rx_cv_.notify_all();
+    }
+
 private:
+    // sub-batch bounds of send_batch (payload bytes, frames) and receive ring buffers: a host
+    // pipeline call costs ~0.3 ms however small (tools/host_rate.cpp: 8 MiB per call runs at
+    // 10 GB/s, 32 MiB at 17, 64 MiB at 21), so calls are made large and the threads overlap
+    // whole calls with the socket
+    static constexpr uint64_t kSubBytes = 64ull << 20;
+    static constexpr size_t kSubFrames = 16384;
+    static constexpr size_t kRing = 3;
+    static constexpr uint64_t kRxBytes = 32ull << 20;
+    static constexpr size_t kRxFrames = 16384;
+    static constexpr size_t kRxMax = 16;  // receive buffers at most (32 MiB of frames each)
+    static constexpr uint64_t kRxEager = 4ull << 20;  // an idle decoder gets a buffer once it holds this much
+
     // largest frame a <= payload-byte message can arrive as (TDT bound or UNCP n + 4)
     size_t frame_capacity(size_t payload) const { return tdt_encode_bound(payload, codec_.word_size()) + 64; }
+
+    // ---- sender ring
+    struct TxBuf {
+        PinnedBuffer mem;
+        std::vector<uint64_t> off;
+        std::vector<int32_t> st;
+        size_t n = 0;
+        bool free = true;
+    };
+    TxBuf &tx_acquire() {
+        std::unique_lock<std::mutex> lk(tx_mu_);
+        for (;;) {
+            if (tx_err_) {
+                lk.unlock();
+                rethrow_tx();
+            }
+            for (auto &b : tx_ring_)
+                if (b.free) {
+                    b.free = false;
+                    return b;
+                }
+            tx_cv_.wait(lk);
+        }
+    }
+    void tx_release_unused(TxBuf &b) {
+        std::lock_guard<std::mutex> lk(tx_mu_);
+        b.free = true;
+    }
+    void tx_submit(TxBuf &b) {
+        {
+            std::lock_guard<std::mutex> lk(tx_mu_);
+            tx_queue_.push_back(&b);
+        }
+        tx_cv_.notify_all();
+    }
+    void rethrow_tx() {
+        std::exception_ptr e;
+        {
+            std::lock_guard<std::mutex> lk(tx_mu_);
+            e = tx_err_;
+            tx_err_ = nullptr;
+        }
+        if (e) std::rethrow_exception(e);
+    }
+    void tx_loop() {
+        for (;;) {
+            TxBuf *b = nullptr;
+            {
+                std::unique_lock<std::mutex> lk(tx_mu_);
+                tx_cv_.wait(lk, [&] { return tx_stop_ || !tx_queue_.empty(); });
+                if (tx_queue_.empty()) return;  // (stop)
+                b = tx_queue_.front();
+                tx_queue_.erase(tx_queue_.begin());
+                tx_busy_ = true;
+            }
+            try {
+                for (size_t k = 0; k < b->n; ++k)
+                    inner_.transport_send(b->mem.data() + b->off[k], b->off[k + 1] - b->off[k]);
+            } catch (...) {
+                std::lock_guard<std::mutex> lk(tx_mu_);
+                tx_err_ = std::current_exception();
+                for (TxBuf *q : tx_queue_) q->free = true;  // frames after a failed send are dropped
+                tx_queue_.clear();
+            }
+            {
+                std::lock_guard<std::mutex> lk(tx_mu_);
+                b->free = true;
+                tx_busy_ = false;
+            }
+            tx_cv_.notify_all();
+        }
+    }
+
+    // ---- receive pipeline: ring buffers move free -> filling -> sealed -> decoded -> free
+    struct RxBuf {
+        PinnedBuffer mem;              // frames back to back
+        std::vector<uint64_t> off{0};  // frame k = mem[off[k] .. off[k+1])
+        PinnedBuffer dec;              // decoded payloads back to back
+        std::vector<uint64_t> doff;    // payload k = dec[doff[k] .. doff[k+1])
+        std::vector<int64_t> claim;    // decoded size each frame's header claims (-1: unreadable)
+        std::vector<int32_t> st;
+        size_t n = 0, used = 0;        // frames received / consumed
+        uint64_t lim = 0;              // frames claiming more were not decoded (the decoder's limit)
+        bool sealed = false, decoded = false, free = true;
+    };
+    // the oldest decoded buffer with unconsumed frames (rx_mu_ held), or null
+    RxBuf *rx_front_decoded() {
+        if (rx_order_.empty()) return nullptr;
+        RxBuf *b = rx_order_.front();
+        return b->decoded && b->used < b->n ? b : nullptr;
+    }
+    // nothing decoded or still to decode is waiting (rx_mu_ held)
+    bool rx_drained() {
+        for (RxBuf *b : rx_order_)
+            if (b->sealed && b->used < b->n) return false;
+        return true;
+    }
+    bool frames_ready() {
+        if (!rx_thread_.joinable()) return false;
+        std::lock_guard<std::mutex> lk(rx_mu_);
+        return rx_front_decoded() != nullptr;
+    }
+    // k frames of the front buffer consumed (rx_mu_ held)
+    void rx_consume(size_t k) { rx_order_.front()->used += k; }
+    // a fully consumed buffer returns to the ring (rx_mu_ held)
+    void rx_release_if_done(RxBuf *b) {
+        if (b->used == b->n && !rx_order_.empty() && rx_order_.front() == b) {
+            rx_order_.erase(rx_order_.begin());
+            b->free = true;
+        }
+    }
+    // views [j0, j1) of the current receive_batch_views call point into buffer b (frames from k0)
+    struct Hold {
+        RxBuf *b;
+        size_t j0, j1, k0;
+    };
+    std::vector<Hold> holds_;
+    // copy the payloads of every fully consumed buffer the current views hold into late_ and
+    // return those buffers to the pipeline
+    template <class V>
+    void migrate_views(V &v) {
+        std::vector<RxBuf *> moved;
+        {
+            std::lock_guard<std::mutex> lk(rx_mu_);
+            moved = rx_held_;
+        }
+        for (Hold &h : holds_) {
+            RxBuf *b = h.b;
+            if (!b || std::find(moved.begin(), moved.end(), b) == moved.end()) continue;
+            const uint64_t a0 = b->doff[h.k0], len = b->doff[h.k0 + (h.j1 - h.j0)] - a0;
+            late_.emplace_back(std::max<uint64_t>(len, 1));
+            if (len) std::memcpy(late_.back().data(), b->dec.data() + a0, len);
+            const uint8_t *lo = b->dec.data() + a0, *hi = lo + len;
+            for (size_t j = h.j0; j < h.j1; ++j)
+                if (v[j].data >= lo && v[j].data < hi) v[j].data = late_.back().data() + (v[j].data - lo);
+            h.b = nullptr;
+        }
+        std::lock_guard<std::mutex> lk(rx_mu_);
+        for (RxBuf *b : moved) b->free = true;
+        rx_held_.erase(std::remove_if(rx_held_.begin(), rx_held_.end(),
+                                      [&](RxBuf *b) { return std::find(moved.begin(), moved.end(), b) != moved.end(); }),
+                       rx_held_.end());
+        rx_cv_.notify_all();
+    }
+    void start_rx(size_t max_msg) {
+        {
+            std::lock_guard<std::mutex> lk(rx_mu_);
+            rx_frame_cap_ = std::max(rx_frame_cap_, frame_capacity(max_msg));
+            rx_max_msg_ = std::max<uint64_t>(rx_max_msg_, max_msg);
+        }
+        if (!rx_thread_.joinable()) {
+            dec_thread_ = std::thread([this] { dec_loop(); });
+            rx_thread_ = std::thread([this] { rx_loop(); });
+        }
+    }
+    // the front buffer once decoded (waits); rethrows the pipeline's error when nothing is left
+    RxBuf *wait_front() {
+        std::unique_lock<std::mutex> lk(rx_mu_);
+        rx_cv_.wait(lk, [&] { return rx_front_decoded() != nullptr || (rx_err_ && rx_drained()); });
+        RxBuf *b = rx_front_decoded();
+        if (!b) std::rethrow_exception(rx_err_);
+        return b;
+    }
+
+    void rx_loop() {
+        for (;;) {
+            RxBuf *b = nullptr;
+            size_t fcap;
+            {
+                std::unique_lock<std::mutex> lk(rx_mu_);
+                // a free buffer of the pool, or a new one while the pool is below kRxMax (a
+                // consumer holding views can keep many buffers at once)
+                auto pick = [&]() -> RxBuf * {
+                    for (auto &q : rx_pool_)
+                        if (q->free) return q.get();
+                    if (rx_pool_.size() < kRxMax) {
+                        rx_pool_.push_back(std::make_unique<RxBuf>());
+                        return rx_pool_.back().get();
+                    }
+                    return nullptr;
+                };
+                rx_cv_.wait(lk, [&] {
+                    if (rx_stop_ || rx_err_) return true;
+                    return (b = pick()) != nullptr;
+                });
+                if (rx_stop_ || rx_err_) return;
+                b->free = false;
+                b->sealed = b->decoded = false;
+                b->n = b->used = 0;
+                b->off.assign(1, 0);
+                rx_order_.push_back(b);
+                fcap = rx_frame_cap_;
+            }
+            b->mem.reserve(std::max<uint64_t>(kRxBytes + fcap, 2 * fcap));
+            auto pause = std::chrono::microseconds(1);
+            auto last = std::chrono::steady_clock::now();
+            for (;;) {
+                size_t flen = 0;
+                bool got = false;
+                if (b->mem.capacity() - b->off[b->n] >= fcap)
+                    got = inner_.try_transport_receive(b->mem.data() + b->off[b->n], fcap, flen);
+                if (got) {
+                    b->off.push_back(b->off[b->n] + flen);
+                    ++b->n;
+                    pause = std::chrono::microseconds(1);
+                    last = std::chrono::steady_clock::now();
+                    if (b->n < kRxFrames && b->off[b->n] < kRxBytes) continue;
+                }
+                if (b->n > 0) {
+                    // full, or the decoder waits for work and either enough has collected or
+                    // the socket has been quiet for a moment: publish (frames keep collecting
+                    // otherwise: larger decode calls)
+                    std::lock_guard<std::mutex> lk(rx_mu_);
+                    const bool full = b->n >= kRxFrames || b->off[b->n] >= kRxBytes ||
+                                      b->mem.capacity() - b->off[b->n] < fcap;
+                    const bool quiet = std::chrono::steady_clock::now() - last > std::chrono::microseconds(20);
+                    if (full || (dec_idle_ && (b->off[b->n] >= kRxEager || quiet))) {
+                        b->sealed = true;
+                        break;
+                    }
+                }
+                bool stop;
+                {
+                    std::lock_guard<std::mutex> lk(rx_mu_);
+                    stop = rx_stop_;
+                    if constexpr (requires(Inner &s) { s.is_connected(); }) {
+                        if (!stop && !inner_.is_connected())
+                            rx_err_ = std::make_exception_ptr(std::runtime_error("TCP: Not connected"));
+                    }
+                    stop = stop || rx_err_ != nullptr;
+                    if (stop) {
+                        if (b->n > 0) {
+                            b->sealed = true;  // what arrived before the end is still delivered
+                        } else {
+                            rx_order_.pop_back();
+                            b->free = true;
+                        }
+                    }
+                }
+                if (stop) {
+                    rx_cv_.notify_all();
+                    return;
+                }
+                std::this_thread::sleep_for(pause);
+                if (pause < std::chrono::microseconds(100)) pause *= 2;
+            }
+            rx_cv_.notify_all();
+        }
+    }
+    // decoder thread: each sealed buffer's frames on the GPU, in arrival order
+    void dec_loop() {
+        for (;;) {
+            RxBuf *b = nullptr;
+            uint64_t lim;
+            {
+                std::unique_lock<std::mutex> lk(rx_mu_);
+                auto next = [&]() -> RxBuf * {
+                    for (RxBuf *q : rx_order_)
+                        if (q->sealed && !q->decoded) return q;
+                    return nullptr;
+                };
+                dec_idle_ = next() == nullptr;
+                rx_cv_.wait(lk, [&] { return rx_stop_ || next() != nullptr; });
+                dec_idle_ = false;
+                if (rx_stop_) return;
+                b = next();
+                lim = rx_max_msg_;
+            }
+            b->claim.resize(b->n);
+            b->st.assign(b->n, TDT_OK);
+            b->doff.assign(b->n + 1, 0);
+            uint64_t total = 0;
+            for (size_t k = 0; k < b->n; ++k) {
+                b->claim[k] = tdt_claimed_size(b->mem.data() + b->off[k], b->off[k + 1] - b->off[k]);
+                if (b->claim[k] > 0 && b->claim[k] <= (int64_t)lim) total += (uint64_t)b->claim[k];
+            }
+            b->dec.reserve(std::max<uint64_t>(total, 1));
+            try {
+                // runs of frames within the limit: one decode call each (a frame claiming more is
+                // never decoded: TDT_E_CAPACITY, no payload)
+                uint64_t o = 0;
+                for (size_t a = 0; a < b->n;) {
+                    if (b->claim[a] > (int64_t)lim) {
+                        b->st[a] = TDT_E_CAPACITY;
+                        b->doff[a + 1] = o;
+                        ++a;
+                        continue;
+                    }
+                    size_t e = a;
+                    uint64_t t = 0;
+                    while (e < b->n && b->claim[e] <= (int64_t)lim) {
+                        if (b->claim[e] > 0) t += (uint64_t)b->claim[e];
+                        ++e;
+                    }
+                    dec_off_.assign(e - a + 1, 0);
+                    if (tdt_decode_host(codec_.context(), b->mem.data(), b->off.data() + a, (uint32_t)(e - a),
+                                        b->dec.data() + o, t, dec_off_.data(), b->st.data() + a) != TDT_OK)
+                        throw std::runtime_error(std::string("TDT: GPU batch decode failed: ") + tdt_last_error());
+                    for (size_t k = a; k < e; ++k) b->doff[k + 1] = o + dec_off_[k - a + 1];
+                    o += dec_off_[e - a];
+                    a = e;
+                }
+            } catch (...) {
+                std::lock_guard<std::mutex> lk(rx_mu_);
+                rx_err_ = std::current_exception();
+                rx_cv_.notify_all();
+                return;
+            }
+            {
+                std::lock_guard<std::mutex> lk(rx_mu_);
+                b->lim = lim;
+                b->decoded = true;
+            }
+            rx_cv_.notify_all();
+        }
+    }
 
     Inner inner_;
     HipTDTCompressionProtocol codec_;
     std::string name_;
-    std::vector<uint8_t> stage_, pack_, enc_;
-    std::vector<uint64_t> eoff_;
+    std::vector<uint8_t> stage_, enc_;
+    std::vector<uint64_t> eoff_, dec_off_;
     size_t raw_sent_ = 0, wire_sent_ = 0, last_received_ = 0;
+    bool record_last_ = false;
+
+    std::mutex tx_mu_;
+    std::condition_variable tx_cv_;
+    TxBuf tx_ring_[kRing];
+    std::vector<TxBuf *> tx_queue_;
+    bool tx_busy_ = false, tx_stop_ = false;
+    std::exception_ptr tx_err_;
+    std::thread tx_thread_;
+
+    std::mutex rx_mu_;
+    std::condition_variable rx_cv_;
+    std::vector<std::unique_ptr<RxBuf>> rx_pool_;
+    std::vector<RxBuf *> rx_held_;            // consumed buffers whose payloads the last views reference
+    std::vector<std::vector<uint8_t>> late_;  // payloads decoded at delivery for the last views
+    std::vector<RxBuf *> rx_order_;  // buffers in arrival order (the one being filled last)
+    size_t rx_frame_cap_ = 0;
+    uint64_t rx_max_msg_ = 0;        // largest max_msg of a receive_batch call: the decoder's limit
+    bool rx_stop_ = false, dec_idle_ = true;
+    std::exception_ptr rx_err_;
+    std::thread rx_thread_, dec_thread_;
 };
 
 }  // namespace psyne_amd

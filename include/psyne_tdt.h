@@ -173,6 +173,19 @@ int tdt_encode_host(tdt_ctx *ctx, const uint8_t *h_in, const uint64_t *h_in_off,
                     uint8_t *h_out, uint64_t out_cap, uint64_t *h_out_off, int32_t *h_status);
 int tdt_decode_host(tdt_ctx *ctx, const uint8_t *h_in, const uint64_t *h_in_off, uint32_t n_msgs,
                     uint8_t *h_out, uint64_t out_cap, uint64_t *h_out_off, int32_t *h_status);
+/* tdt_encode_host over n messages that are NOT contiguous (message i = msgs[i][0 .. sizes[i])),
+ * as a substrate's send path holds them (one buffer per message, transport_send(void*, size_t),
+ * tcp_simple.hpp:68-91): the pool copies them straight into the pinned staging, no packing
+ * copy.  Replaces a loop of TDTCompressionProtocol::encode (tdt_compression.hpp:227-266). */
+int tdt_encode_host_v(tdt_ctx *ctx, const uint8_t *const *msgs, const uint64_t *sizes, uint32_t n_msgs,
+                      uint8_t *h_out, uint64_t out_cap, uint64_t *h_out_off, int32_t *h_status);
+/* Pinned (page-locked, device-mapped) host memory for callers that keep their socket buffers in
+ * it: the host paths DMA such buffers directly instead of staging them.  Returns TDT_OK. */
+int tdt_host_alloc(uint64_t bytes, void **ptr);
+void tdt_host_free(void *ptr);
+/* dst[0, bytes) = src[0, bytes) on the context's staging-copy threads (a parallel memcpy: one
+ * thread's copy is below what a socket pipeline needs).  Host memory only. */
+int tdt_host_copy(tdt_ctx *ctx, void *dst, const void *src, uint64_t bytes);
 
 /* Device-side invariant flags: bit0 look-back timeout, bit1 staging-index guard, bit2
  * flush-bound guard.  Always 0 for a correct build; the guards turn a logic error into a flag

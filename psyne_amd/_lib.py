@@ -50,6 +50,10 @@ SIGNATURES = {
     "tdt_analyze_batch": (C.c_int, [_vp, _vp, _vp, C.c_uint32, _vp, _vp, _vp, _vp, _vp]),
     "tdt_encode_host": (C.c_int, [_vp, _vp, _vp, C.c_uint32, _vp, C.c_uint64, _vp, _vp]),
     "tdt_decode_host": (C.c_int, [_vp, _vp, _vp, C.c_uint32, _vp, C.c_uint64, _vp, _vp]),
+    "tdt_encode_host_v": (C.c_int, [_vp, _vp, _vp, C.c_uint32, _vp, C.c_uint64, _vp, _vp]),
+    "tdt_host_alloc": (C.c_int, [C.c_uint64, C.POINTER(C.c_void_p)]),
+    "tdt_host_free": (None, [_vp]),
+    "tdt_host_copy": (C.c_int, [_vp, _vp, _vp, C.c_uint64]),
     "tdt_analyze_host": (C.c_int, [_vp, _vp, _vp, C.c_uint32, _vp, _vp, _vp]),
     "tdt_ctx_error_flags": (C.c_int, [_vp, _vp, C.POINTER(C.c_uint32)]),
     "tdt_ctx_set_option": (C.c_int, [_vp, C.c_int, C.c_uint64]),

@@ -170,7 +170,16 @@ struct tdt_ctx {
         hipEvent_t evc = nullptr;  // after the chunk's output copy (orders the next chunk's)
         PlanWS pw;
     } hs[2];
-    std::unique_ptr<CopyPool> pool;  // host threads of the staging copies
+    // one-message fast path (tdt_encode_host / tdt_decode_host with one message of at most
+    // kOneMax bytes: the per-call Protocol::encode / decode of the drop-in class): a mapped pinned
+    // block holding the call's offsets, list, status, input and output, read and written by ONE
+    // class kernel in place (zero-copy), so a call is two host memcpys, one launch and one sync
+    uint8_t *one = nullptr;
+    size_t one_bytes = 0;
+    hipStream_t one_stream = nullptr;
+    uint8_t *one_dev = nullptr;  // device copy of a larger blob (one-wave decode reads it from HBM)
+    size_t one_dev_bytes = 0;
+    std::shared_ptr<CopyPool> pool;  // host threads of the staging copies (shared: tdt_host_copy)
     uint64_t *hbases = nullptr;      // host_encode: device-side running output base per chunk
     size_t hbases_n = 0;
     int copy_threads = 8;
@@ -190,6 +199,7 @@ struct tdt_ctx {
     bool no_side = false;       // PSYNE_TDT_NO_SIDE: no side stream for the tile pipeline
     bool small_main = false;    // PSYNE_TDT_SMALL_MAIN: small lists on the caller's stream
     bool no_two_phase = false;  // PSYNE_TDT_NO_TWO_PHASE: compacted calls take the one-pass kernels
+    bool no_one = false;        // PSYNE_TDT_NO_ONE: one-message host calls take the pipeline too
     uint32_t copy_wgs = 8;      // PSYNE_TDT_COPY_WGS: copy-list workgroups per CU
     // PSYNE_TDT_DSMALL_MAX: blobs decoding to at most this many bytes take the one-round-window
     // list on the side stream (C4 decode 11.80 -> 11.42 ms at 8 KiB against 1 KiB; 16-64 KiB
@@ -972,15 +982,22 @@ struct Chunk {
     size_t o_off = 0, o_out = 0, o_ooff = 0, o_st = 0, o_ws = 0;
 };
 
+// Chunk size of a call: a quarter of its input (so that H2D, kernel and D2H of neighbouring
+// chunks overlap even for a socket-sized batch of tens of MiB), between 4 and 64 MiB.
+uint64_t host_chunk_bytes(const uint64_t *h_in_off, uint32_t n_msgs) {
+    const uint64_t total = h_in_off[n_msgs] - h_in_off[0];
+    return std::min<uint64_t>(kHostChunk, std::max<uint64_t>(4ull << 20, (total / 4 + 4095) & ~4095ull));
+}
+
 Chunk plan_chunk(const uint64_t *h_in_off, uint32_t m0, uint32_t n_msgs, bool encode, int ws,
-                 const uint64_t *dec_sizes) {
+                 const uint64_t *dec_sizes, uint64_t chunk_bytes) {
     Chunk k;
     k.m0 = m0;
     uint32_t m = m0;
     uint64_t cap = 0;
     while (m < n_msgs) {
         const uint64_t len = h_in_off[m + 1] - h_in_off[m];
-        if (m > m0 && h_in_off[m + 1] - h_in_off[m0] > kHostChunk) break;
+        if (m > m0 && h_in_off[m + 1] - h_in_off[m0] > chunk_bytes) break;
         cap += encode ? tdt_encode_bound(len, ws) : dec_sizes[m];
         ++m;
     }
@@ -1046,10 +1063,13 @@ __global__ __launch_bounds__(256) void host_out_kernel(const uint8_t *src, const
     for (uint64_t k = head + 16 * nb + gtid; k < total; k += gsz) d[k] = src[k];
 }
 
+// msgs / sizes (gather input, tdt_encode_host_v): message i = msgs[i][0 .. sizes[i]); h_in is then
+// unused and h_in_off holds the prefix sums of sizes
 int host_encode(tdt_ctx *c, const uint8_t *h_in, const uint64_t *h_in_off, uint32_t n_msgs, uint8_t *h_out,
-                uint64_t out_cap, uint64_t *h_out_off, int32_t *h_status) {
+                uint64_t out_cap, uint64_t *h_out_off, int32_t *h_status, const uint8_t *const *msgs = nullptr,
+                const uint64_t *sizes = nullptr) {
     const int ws = c->cfg.word_size;
-    const bool pin_in = is_pinned(h_in + h_in_off[0]);
+    const bool pin_in = !msgs && is_pinned(h_in + h_in_off[0]);
     // a pinned caller buffer receives the chunks' output straight from the copy kernels
     uint8_t *d_out = nullptr;
     if (is_pinned(h_out) && hipHostGetDevicePointer(reinterpret_cast<void **>(&d_out), h_out, 0) != hipSuccess) {
@@ -1058,8 +1078,9 @@ int host_encode(tdt_ctx *c, const uint8_t *h_in, const uint64_t *h_in_off, uint3
     }
     const bool pin_out = d_out != nullptr;
     std::vector<Chunk> ch;
+    const uint64_t cb = host_chunk_bytes(h_in_off, n_msgs);
     for (uint32_t m = 0; m < n_msgs;) {
-        ch.push_back(plan_chunk(h_in_off, m, n_msgs, true, ws, nullptr));
+        ch.push_back(plan_chunk(h_in_off, m, n_msgs, true, ws, nullptr, cb));
         m += ch.back().n;
     }
     if (ch.size() + 1 > c->hbases_n) {
@@ -1081,8 +1102,11 @@ int host_encode(tdt_ctx *c, const uint8_t *h_in, const uint64_t *h_in_off, uint3
         uint64_t *pin_in_off = h.pin;
         const uint64_t b0 = h_in_off[k.m0];
         for (uint32_t i = 0; i <= k.n; ++i) pin_in_off[i] = h_in_off[k.m0 + i] - b0;
-        const uint8_t *src = h_in + b0;
-        if (!pin_in) {
+        const uint8_t *src = msgs ? nullptr : h_in + b0;
+        if (msgs) {
+            c->pool->gather(h.stage_in, msgs + k.m0, sizes + k.m0, k.n);
+            src = h.stage_in;
+        } else if (!pin_in) {
             c->pool->copy(h.stage_in, src, k.in_bytes);
             src = h.stage_in;
         }
@@ -1153,8 +1177,9 @@ int host_decode(tdt_ctx *c, const uint8_t *h_in, const uint64_t *h_in_off, uint3
     const bool pin_in = is_pinned(h_in + h_in_off[0]), pin_out = is_pinned(h_out);
     std::vector<Chunk> ch;
     uint64_t base = 0;
+    const uint64_t cb = host_chunk_bytes(h_in_off, n_msgs);
     for (uint32_t m = 0; m < n_msgs;) {
-        ch.push_back(plan_chunk(h_in_off, m, n_msgs, false, c->cfg.word_size, dsz.data()));
+        ch.push_back(plan_chunk(h_in_off, m, n_msgs, false, c->cfg.word_size, dsz.data(), cb));
         ch.back().base = base;
         base += ch.back().cap;
         m += ch.back().n;
@@ -1235,6 +1260,147 @@ int host_decode(tdt_ctx *c, const uint8_t *h_in, const uint64_t *h_in_off, uint3
     return TDT_OK;
 }
 
+// ---------------------------------------------------------------------------------------
+// One-message fast path.  Block layout (`one`, mapped pinned memory): [0, 256) argument words,
+// then the input at kOneIn, then the output.  The class kernel of the message's size runs as a
+// single workgroup on a one-entry list; every argument, the input and the output live in host
+// memory the kernel reads and writes over PCIe.
+constexpr uint64_t kOneMax = 256 * 1024;  // largest message (encode) / decoded message the path takes
+constexpr size_t kOneIn = 256;
+constexpr uint64_t kOneDevMin = 16 * 1024;  // decode: blobs above this are copied to HBM first
+struct OneArgs {
+    uint64_t off[2];   // input offsets
+    uint64_t slot[2];  // output slot
+    uint64_t len;      // output length
+    int32_t status;
+    uint32_t list, cnt, flags;
+};
+
+int ensure_one(tdt_ctx *c, size_t bytes) {
+    if (!c->one_stream) HIPCHK(hipStreamCreateWithFlags(&c->one_stream, hipStreamNonBlocking));
+    if (bytes <= c->one_bytes) return TDT_OK;
+    if (c->one) HIPCHK(hipHostFree(c->one));
+    c->one = nullptr;
+    c->one_bytes = 0;
+    const size_t cap = std::max<size_t>(bytes, 64 * 1024);
+    HIPCHK(hipHostMalloc(&c->one, cap, hipHostMallocDefault));
+    c->one_bytes = cap;
+    return TDT_OK;
+}
+
+template <int WS>
+void launch_one_encode(const psy::EncodeArgs &a, uint64_t n, hipStream_t s) {
+    using psy::MODE_ENCODE;
+    if (n <= kSmallMax)
+        hipLaunchKernelGGL((psy::tdt_encode_kernel<WS, 64, 4, MODE_ENCODE, 0, 0, 0>), dim3(1), dim3(64), 0, s, a);
+    else if (n <= kMidMax)
+        hipLaunchKernelGGL((psy::tdt_encode_kernel<WS, 256, 8, MODE_ENCODE, 0, 0, 0>), dim3(1), dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL((psy::tdt_encode_kernel<WS, 512, 8, MODE_ENCODE, 0, 0, 0>), dim3(1), dim3(512), 0, s, a);
+}
+
+// returns TDT_OK, an error, or -1: not taken (the pipeline serves the call)
+int host_one(tdt_ctx *c, bool encode, const uint8_t *h_in, const uint64_t *h_in_off, uint8_t *h_out,
+             uint64_t out_cap, uint64_t *h_out_off, int32_t *h_status) {
+    const uint64_t len = h_in_off[1] - h_in_off[0];
+    const uint8_t *src = h_in + h_in_off[0];
+    uint64_t osize;
+    if (encode) {
+        if (len > kOneMax) return -1;
+        osize = tdt_encode_bound(len, c->cfg.word_size);
+    } else {
+        osize = host_decoded_size(src, len);
+        if (osize > kOneMax || len > 2 * kOneMax + 1024) return -1;
+        if (osize > out_cap) return set_err(TDT_E_CAPACITY, "host output capacity exceeded");
+    }
+    const size_t o_out = kOneIn + align_up(std::max<uint64_t>(len, 1), 256);
+    int st = ensure_one(c, o_out + align_up(std::max<uint64_t>(osize, 1), 256) + 256);
+    if (st) return st;
+    uint8_t *hb = c->one;
+    uint8_t *db = nullptr;
+    HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void **>(&db), hb, 0));
+    OneArgs *A = reinterpret_cast<OneArgs *>(hb);
+    const OneArgs *dA = reinterpret_cast<const OneArgs *>(db);
+    A->off[0] = 0;
+    A->off[1] = len;
+    A->slot[0] = 0;
+    A->slot[1] = osize;
+    A->len = 0;
+    A->status = -1;
+    A->list = 0;
+    A->cnt = 1;
+    A->flags = 0;
+    if (len) std::memcpy(hb + kOneIn, src, len);
+    hipStream_t s = c->one_stream;
+    if (encode) {
+        psy::EncodeArgs a{};
+        a.in = db + kOneIn;
+        a.in_off = dA->off;
+        a.n_msgs = 1;
+        a.out = db + o_out;
+        a.slot_off = dA->slot;
+        a.out_len = const_cast<uint64_t *>(&dA->len);
+        a.status = const_cast<int32_t *>(&dA->status);
+        a.errflags = const_cast<uint32_t *>(&dA->flags);
+        a.min_tensor = c->cfg.min_tensor_size;
+        a.policy_on = policy_on(c) ? 1 : 0;
+        a.list = &dA->list;
+        a.list_count = &dA->cnt;
+        switch (c->cfg.word_size) {
+#ifdef PSY_FAST_BUILD
+            case 4: launch_one_encode<4>(a, len, s); break;
+#else
+            case 1: launch_one_encode<1>(a, len, s); break;
+            case 2: launch_one_encode<2>(a, len, s); break;
+            case 4: launch_one_encode<4>(a, len, s); break;
+            case 8: launch_one_encode<8>(a, len, s); break;
+            case 16: launch_one_encode<16>(a, len, s); break;
+#endif
+            default: return set_err(TDT_E_UNSUPPORTED, "word_size not supported on the GPU path");
+        }
+    } else {
+        psy::DecodeArgs a{};
+        a.in = db + kOneIn;
+        if (len > kOneDevMin) {
+            // one wave walks the blob window by window: its pair loads are dependent, so they come
+            // from HBM (one DMA of the blob) rather than over PCIe one window at a time
+            if (len > c->one_dev_bytes) {
+                if (c->one_dev) HIPCHK(hipFree(c->one_dev));
+                c->one_dev = nullptr;
+                c->one_dev_bytes = 0;
+                HIPCHK(hipMalloc(&c->one_dev, std::max<size_t>(len, 256 * 1024)));
+                c->one_dev_bytes = std::max<size_t>(len, 256 * 1024);
+            }
+            HIPCHK(hipMemcpyAsync(c->one_dev, hb + kOneIn, len, hipMemcpyHostToDevice, s));
+            a.in = c->one_dev;
+        }
+        a.in_off = dA->off;
+        a.n_msgs = 1;
+        a.out = db + o_out;
+        a.slot_off = dA->slot;
+        a.out_len = const_cast<uint64_t *>(&dA->len);
+        a.status = const_cast<int32_t *>(&dA->status);
+        a.errflags = const_cast<uint32_t *>(&dA->flags);
+        a.list = &dA->list;
+        a.list_count = &dA->cnt;
+        hipLaunchKernelGGL((psy::tdt_decode_kernel<0, psy::kDecWR, 0>), dim3(1), dim3(64), 0, s, a);
+    }
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(s));
+    c->host_flags.fetch_or(A->flags);
+    const uint64_t olen = A->len;
+    const int32_t ost = A->status;
+    if (h_status) h_status[0] = ost;
+    h_out_off[0] = 0;
+    if (encode && olen > out_cap) {
+        h_out_off[1] = 0;
+        return set_err(TDT_E_CAPACITY, "host output capacity exceeded");
+    }
+    if (olen) std::memcpy(h_out, hb + o_out, olen);
+    h_out_off[1] = olen;
+    return TDT_OK;
+}
+
 int host_path(tdt_ctx *c, bool encode, const uint8_t *h_in, const uint64_t *h_in_off, uint32_t n_msgs,
               uint8_t *h_out, uint64_t out_cap, uint64_t *h_out_off, int32_t *h_status) {
     if (!c) return set_err(TDT_E_ARG, "null context");
@@ -1245,6 +1411,10 @@ int host_path(tdt_ctx *c, bool encode, const uint8_t *h_in, const uint64_t *h_in
     if (!h_in_off || !h_out_off) return set_err(TDT_E_ARG, "null offsets");
     HIPCHK(hipSetDevice(c->device));
     std::lock_guard<std::mutex> lk(c->hmu);  // the pipeline slots belong to the context
+    if (n_msgs == 1 && !c->no_one) {
+        const int st1 = host_one(c, encode, h_in, h_in_off, h_out, out_cap, h_out_off, h_status);
+        if (st1 >= 0) return st1;
+    }
     if (!c->pool) c->pool.reset(new CopyPool(c->copy_threads));
     const int st = encode ? host_encode(c, h_in, h_in_off, n_msgs, h_out, out_cap, h_out_off, h_status)
                           : host_decode(c, h_in, h_in_off, n_msgs, h_out, out_cap, h_out_off, h_status);
@@ -1358,6 +1528,7 @@ int tdt_ctx_create(int device, const tdt_config *cfg, tdt_ctx **out) {
     x->no_side = flag("PSYNE_TDT_NO_SIDE");
     x->small_main = flag("PSYNE_TDT_SMALL_MAIN");
     x->no_two_phase = flag("PSYNE_TDT_NO_TWO_PHASE");
+    x->no_one = flag("PSYNE_TDT_NO_ONE");
     if (const char *e = std::getenv("PSYNE_TDT_DBIG_MIN")) x->dbig_min = std::strtoull(e, nullptr, 10);
     if (const char *e = std::getenv("PSYNE_TDT_DSMALL_MAX")) x->dsmall_max = std::strtoull(e, nullptr, 10);
     if (const char *e = std::getenv("PSYNE_TDT_COPY_WGS")) x->copy_wgs = std::max(1ul, std::strtoul(e, nullptr, 10));
@@ -1384,6 +1555,10 @@ void tdt_ctx_destroy(tdt_ctx *ctx) {
     for (void *p : ctx->retired) (void)hipFree(p);
     ctx->pw.release();
     if (ctx->hbases) (void)hipFree(ctx->hbases);
+    if (ctx->one_stream) (void)hipStreamSynchronize(ctx->one_stream);
+    if (ctx->one) (void)hipHostFree(ctx->one);
+    if (ctx->one_dev) (void)hipFree(ctx->one_dev);
+    if (ctx->one_stream) (void)hipStreamDestroy(ctx->one_stream);
     if (ctx->astream) (void)hipStreamSynchronize(ctx->astream);
     if (ctx->h_dev) (void)hipFree(ctx->h_dev);
     if (ctx->astream) (void)hipStreamDestroy(ctx->astream);
@@ -1617,6 +1792,55 @@ int tdt_encode_host(tdt_ctx *ctx, const uint8_t *h_in, const uint64_t *h_in_off,
 int tdt_decode_host(tdt_ctx *ctx, const uint8_t *h_in, const uint64_t *h_in_off, uint32_t n_msgs, uint8_t *h_out,
                     uint64_t out_cap, uint64_t *h_out_off, int32_t *h_status) {
     return host_path(ctx, false, h_in, h_in_off, n_msgs, h_out, out_cap, h_out_off, h_status);
+}
+
+int tdt_encode_host_v(tdt_ctx *ctx, const uint8_t *const *msgs, const uint64_t *sizes, uint32_t n_msgs, uint8_t *h_out,
+                      uint64_t out_cap, uint64_t *h_out_off, int32_t *h_status) {
+    if (!ctx) return set_err(TDT_E_ARG, "null context");
+    if (n_msgs == 0) {
+        if (h_out_off) h_out_off[0] = 0;
+        return TDT_OK;
+    }
+    if (!msgs || !sizes || !h_out_off) return set_err(TDT_E_ARG, "null argument");
+    if (n_msgs == 1) {
+        const uint64_t off[2] = {0, sizes[0]};
+        return host_path(ctx, true, msgs[0], off, 1, h_out, out_cap, h_out_off, h_status);
+    }
+    std::vector<uint64_t> voff(n_msgs + 1, 0);
+    for (uint32_t i = 0; i < n_msgs; ++i) voff[i + 1] = voff[i] + sizes[i];
+    HIPCHK(hipSetDevice(ctx->device));
+    std::lock_guard<std::mutex> lk(ctx->hmu);
+    if (!ctx->pool) ctx->pool.reset(new CopyPool(ctx->copy_threads));
+    const int st = host_encode(ctx, nullptr, voff.data(), n_msgs, h_out, out_cap, h_out_off, h_status, msgs, sizes);
+    if (st != TDT_OK) {
+        for (auto &h : ctx->hs)
+            if (h.stream) (void)hipStreamSynchronize(h.stream);
+        (void)hipGetLastError();
+    }
+    return st;
+}
+
+int tdt_host_alloc(uint64_t bytes, void **ptr) {
+    if (!ptr) return set_err(TDT_E_ARG, "null argument");
+    *ptr = nullptr;
+    HIPCHK(hipHostMalloc(ptr, std::max<uint64_t>(bytes, 1), hipHostMallocDefault));
+    return TDT_OK;
+}
+
+void tdt_host_free(void *ptr) {
+    if (ptr) (void)hipHostFree(ptr);
+}
+
+int tdt_host_copy(tdt_ctx *ctx, void *dst, const void *src, uint64_t bytes) {
+    if (!ctx || (bytes && (!dst || !src))) return set_err(TDT_E_ARG, "null argument");
+    std::shared_ptr<CopyPool> pool;
+    {
+        std::lock_guard<std::mutex> lk(ctx->hmu);  // (the pool is created and replaced under hmu)
+        if (!ctx->pool) ctx->pool.reset(new CopyPool(ctx->copy_threads));
+        pool = ctx->pool;
+    }
+    pool->copy(dst, src, bytes);  // (outside hmu: CopyPool::copy serialises concurrent callers itself)
+    return TDT_OK;
 }
 
 int tdt_ctx_error_flags(tdt_ctx *ctx, void *stream, uint32_t *flags) {

@@ -80,6 +80,74 @@ class CopyPool {
         job->s = static_cast<const uint8_t *>(src);
         job->bytes = bytes;
         job->parts = std::min<size_t>(bytes / kPart + 1, 4 * (th_.size() + 1));
+        submit(job);
+    }
+
+    // Gather: dst = msgs[0][0 .. sizes[0]) ++ msgs[1][...] ++ ... (n messages back to back).
+    // Messages are grouped into pieces of about kPart bytes (a large message is split).
+    void gather(void *dst, const uint8_t *const *msgs, const uint64_t *sizes, size_t n) {
+        uint64_t total = 0;
+        for (size_t i = 0; i < n; ++i) total += sizes[i];
+        if (total < kParMin || th_.empty()) {
+            uint8_t *d = static_cast<uint8_t *>(dst);
+            for (size_t i = 0; i < n; ++i) {
+                std::memcpy(d, msgs[i], sizes[i]);
+                d += sizes[i];
+            }
+            return;
+        }
+        std::lock_guard<std::mutex> one(call_);
+        auto job = std::make_shared<Job>();
+        uint8_t *d = static_cast<uint8_t *>(dst);
+        size_t k = 0;  // first message of the open piece
+        uint64_t acc = 0;
+        for (size_t i = 0; i < n; ++i) {
+            if (sizes[i] >= kPart) {  // a large message: its own pieces
+                if (i > k) job->pieces.push_back({d - acc, nullptr, acc, k, i});
+                for (uint64_t o = 0; o < sizes[i]; o += kPart)
+                    job->pieces.push_back({d + o, msgs[i] + o, std::min<uint64_t>(kPart, sizes[i] - o), 0, 0});
+                d += sizes[i];
+                acc = 0;
+                k = i + 1;
+                continue;
+            }
+            d += sizes[i];
+            acc += sizes[i];
+            if (acc >= kPart) {
+                job->pieces.push_back({d - acc, nullptr, acc, k, i + 1});
+                acc = 0;
+                k = i + 1;
+            }
+        }
+        if (k < n) job->pieces.push_back({d - acc, nullptr, acc, k, n});
+        job->msgs = msgs;
+        job->sizes = sizes;
+        job->parts = job->pieces.size();
+        submit(job);
+    }
+
+  private:
+    static constexpr size_t kParMin = 1u << 20, kPart = 2u << 20;
+    // one copy call; a worker that wakes late holds a finished job and finds no part left
+    // a gather piece: bytes [d, d + len) from src (one message's part), or from messages
+    // [m0, m1) back to back (src null)
+    struct Piece {
+        uint8_t *d;
+        const uint8_t *src;
+        uint64_t len;
+        size_t m0, m1;
+    };
+    struct Job {
+        uint8_t *d = nullptr;
+        const uint8_t *s = nullptr;
+        size_t bytes = 0, parts = 0;
+        std::vector<Piece> pieces;  // gather jobs
+        const uint8_t *const *msgs = nullptr;
+        const uint64_t *sizes = nullptr;
+        std::atomic<size_t> next{0}, left{0};
+    };
+
+    void submit(const std::shared_ptr<Job> &job) {
         job->left.store(job->parts);
         {
             std::lock_guard<std::mutex> lk(m_);
@@ -93,23 +161,26 @@ class CopyPool {
         job_.reset();
     }
 
-  private:
-    static constexpr size_t kParMin = 1u << 20, kPart = 2u << 20;
-    // one copy call; a worker that wakes late holds a finished job and finds no part left
-    struct Job {
-        uint8_t *d = nullptr;
-        const uint8_t *s = nullptr;
-        size_t bytes = 0, parts = 0;
-        std::atomic<size_t> next{0}, left{0};
-    };
-
     void run(Job &j) {
-        const size_t per = (j.bytes + j.parts - 1) / j.parts;
+        const size_t per = j.pieces.empty() ? (j.bytes + j.parts - 1) / j.parts : 0;
         for (;;) {
             const size_t i = j.next.fetch_add(1);
             if (i >= j.parts) return;
-            const size_t b = i * per, e = std::min(j.bytes, b + per);
-            if (b < e) part_copy(j.d + b, j.s + b, e - b);
+            if (!j.pieces.empty()) {
+                const Piece &p = j.pieces[i];
+                if (p.src) {
+                    part_copy(p.d, p.src, p.len);
+                } else {
+                    uint8_t *d = p.d;
+                    for (size_t m = p.m0; m < p.m1; ++m) {
+                        std::memcpy(d, j.msgs[m], j.sizes[m]);
+                        d += j.sizes[m];
+                    }
+                }
+            } else {
+                const size_t b = i * per, e = std::min(j.bytes, b + per);
+                if (b < e) part_copy(j.d + b, j.s + b, e - b);
+            }
             if (j.left.fetch_sub(1) == 1) {
                 std::lock_guard<std::mutex> lk(m_);
                 done_.notify_all();

@@ -9,9 +9,12 @@
 // clock starts (the reference times its generator inside the loop, :342-360):
 //
 //   --codec gpu   TdtSubstrate<PosixTcpSubstrate> on both ends (each owns its socket end and a
-//                 GPU codec context): batches of --batch tensors are encoded by one
-//                 tdt_encode_host call and sent as one frame per blob; the receiver takes
-//                 --batch frames and decodes them with one tdt_decode_host call
+//                 GPU codec context): batches of --batch tensors go through send_batch (encoded
+//                 in sub-batches by tdt_encode_host_v, sent by the decorator's sender thread while
+//                 the next sub-batch is on the GPU); the receiver takes --batch frames per
+//                 receive_batch_views (--rx views, default: payloads checked where the decoder
+//                 left them, in pinned memory) or receive_batch (--rx copy: into a vector); its
+//                 receiver and decoder threads read and decode ahead
 //   --codec cpu   the REFERENCE codec (psyne::protocol::TDTCompressionProtocol compiled where
 //                 it lies: oracle/_ref/libtdt_ref.so, loaded at run time), one protocol object
 //                 per endpoint, one message per encode / decode — psyne's own CPU path
@@ -69,6 +72,12 @@ std::string repo_root(const char *argv0) {
 
 int main(int argc, char **argv) {
     size_t count = 1000, floats = 256 * 1024, batch = 50, warm = 2;
+    // diagnostics of the gpu row's two halves: --half tx (the receiver drains raw frames: no
+    // decode, no check) or --half rx (the sender sends frames encoded before the clock starts)
+    std::string half = "both";
+    // gpu receiver: "views" (receive_batch_views: payloads checked in the pipeline's pinned
+    // buffers, zero-copy) or "copy" (receive_batch into a std::vector)
+    std::string rxmode = "views";
     int port = 18080;
     std::string codec = "gpu", dump;
     for (int i = 1; i + 1 < argc; i += 2) {
@@ -80,6 +89,8 @@ int main(int argc, char **argv) {
         else if (k == "--codec") codec = v;
         else if (k == "--dump") dump = v;
         else if (k == "--warm") warm = std::stoul(v);
+        else if (k == "--half") half = v;
+        else if (k == "--rx") rxmode = v;
     }
     const size_t bytes = floats * 4;
     // payloads (GRADIENTS: 70 % zeros, N(0, 0.01) otherwise)
@@ -136,6 +147,27 @@ int main(int argc, char **argv) {
 
     std::vector<const void *> ptrs(batch);
     std::vector<size_t> sizes(batch, bytes);
+    // --half rx: every batch's frames encoded (by the sender's codec) before the clock starts
+    std::vector<std::vector<uint8_t>> pre;
+    std::vector<std::vector<uint64_t>> pre_off;
+    if (codec == "gpu" && half == "rx") {
+        for (size_t b = 0; b < count; b += batch) {
+            const size_t nb = std::min(batch, count - b);
+            std::vector<const uint8_t *> mp(nb);
+            std::vector<uint64_t> ms(nb, bytes), eo(nb + 1, 0);
+            for (size_t i = 0; i < nb; ++i) mp[i] = msgs[b + i].data();
+            std::vector<uint8_t> enc(nb * tdt_encode_bound(bytes, 4));
+            std::vector<int32_t> est(nb);
+            if (tdt_encode_host_v(tx->codec().context(), mp.data(), ms.data(), (uint32_t)nb, enc.data(), enc.size(),
+                                  eo.data(), est.data()) != TDT_OK) {
+                std::fprintf(stderr, "pre-encode failed: %s\n", tdt_last_error());
+                return 5;
+            }
+            enc.resize(eo[nb]);
+            pre.push_back(std::move(enc));
+            pre_off.push_back(std::move(eo));
+        }
+    }
     std::vector<uint8_t> blob(tdt_encode_bound(bytes, 4));
     size_t wire = 0, mismatches = 0;
     // One pass: tensors [0, n) sent in batches and verified on receipt.  The warm-up pass (not
@@ -148,6 +180,20 @@ int main(int argc, char **argv) {
         std::vector<uint8_t> frame(tdt_encode_bound(bytes, 4) + 64), back(bytes);
         for (size_t b = 0; b < n; b += batch) {
             const size_t nb = std::min(batch, n - b);
+            if (codec == "gpu" && half == "tx") {
+                for (size_t i = 0; i < nb; ++i) {
+                    size_t flen = 0;
+                    while (!rx_inner->try_transport_receive(frame.data(), frame.size(), flen)) std::this_thread::yield();
+                }
+                continue;
+            }
+            if (codec == "gpu" && rxmode == "views") {
+                const auto v = rx->receive_batch_views(nb, bytes);
+                for (size_t i = 0; i < nb; ++i)
+                    if (v[i].status != TDT_OK || v[i].size != bytes || std::memcmp(v[i].data, msgs[b + i].data(), bytes))
+                        ++mismatches;
+                continue;
+            }
             if (codec == "gpu") {
                 const std::vector<int32_t> st = rx->receive_batch(nb, bytes, out, off);
                 for (size_t i = 0; i < nb; ++i)
@@ -175,8 +221,16 @@ int main(int argc, char **argv) {
             }
         }
     });
+    if (codec == "gpu") tx->record_last_batch(frames != nullptr || half == "rx");
     for (size_t b = 0; b < n; b += batch) {
         const size_t nb = std::min(batch, n - b);
+        if (codec == "gpu" && half == "rx") {
+            const std::vector<uint8_t> &enc = pre[b / batch];
+            const std::vector<uint64_t> &eo = pre_off[b / batch];
+            for (size_t i = 0; i < nb; ++i) tx_inner->transport_send((void *)(enc.data() + eo[i]), eo[i + 1] - eo[i]);
+            wire += eo[nb];
+            continue;
+        }
         if (codec == "gpu") {
             for (size_t i = 0; i < nb; ++i) ptrs[i] = msgs[b + i].data();
             wire += tx->send_batch(ptrs.data(), sizes.data(), nb);
@@ -210,6 +264,7 @@ int main(int argc, char **argv) {
             wire += len;
         }
     }
+    if (codec == "gpu" && half != "rx") tx->flush();  // every queued frame is on the wire
     receiver.join();
     };
     if (warm) {
@@ -226,9 +281,9 @@ int main(int argc, char **argv) {
     std::printf("{\"harness\": \"tcp_loopback\", \"codec\": \"%s\", \"tensors\": %zu, \"tensor_bytes\": %zu, "
                 "\"batch\": %zu, \"seconds\": %.4f, \"original_MB\": %.1f, \"wire_MB\": %.1f, "
                 "\"compression_ratio\": %.4f, \"effective_MBps\": %.1f, \"network_MBps\": %.1f, "
-                "\"mismatches\": %zu, \"warmup_tensors\": %zu}\n",
+                "\"mismatches\": %zu, \"warmup_tensors\": %zu, \"half\": \"%s\", \"rx\": \"%s\"}\n",
                 codec.c_str(), count, bytes, codec == "gpu" ? batch : (size_t)1, secs, orig / 1e6,
                 double(wire) / 1e6, orig / double(wire), orig / 1e6 / secs, double(wire) / 1e6 / secs, mismatches,
-                warm ? std::min(count, warm * batch) : (size_t)0);
+                warm ? std::min(count, warm * batch) : (size_t)0, half.c_str(), codec == "gpu" ? rxmode.c_str() : "-");
     return mismatches ? 1 : 0;
 }

@@ -559,3 +559,60 @@ def test_mapping_ties_exact_fallback(orc):
             msgs.append(y.reshape(-1))
     check_vs_oracle(orc, make_codec(), msgs)
     check_vs_oracle(orc, make_codec(hint=1024), msgs)
+
+
+@pytest.mark.parametrize("ws", [4, 8])
+def test_one_message_host_path(orc, ws):
+    """tdt_encode_host / tdt_decode_host with ONE message (the drop-in Protocol::encode / decode
+    call, protocol_demo.cpp:135-189) take the zero-copy one-message path up to 256 KiB: every
+    size class (UNCP, one-wave, 256-lane, 512-lane resident and streaming), odd and unaligned
+    sizes, the 256 KiB bound and just past it (the pipeline), each blob equal to the oracle's and
+    decoded back; corrupted blobs report the reference's errors through the status."""
+    from psyne_amd._lib import TDT_OK
+    rng = np.random.default_rng(90 + ws)
+    codec = make_codec(ws=ws)
+    cfg = orc.config(word_size=ws, sample_fraction=1.0)
+    sizes = [0, 3, 64, 1020, 1024, 1032, 4096, 4104, 8192, 32768, 32776, 65536, 65544, 100000, 131072,
+             262144, 262144 + 8, 1 << 20]
+    for n in sizes:
+        m = grad(rng, n // 4).view(np.uint8) if n % 4 == 0 else rng.integers(0, 256, n, dtype=np.uint8)
+        m = np.ascontiguousarray(m[:n])
+        enc, eoff, st = codec.encode_host(m, np.array([0, n], np.uint64))
+        assert int(st[0]) == TDT_OK, n
+        want = orc.encode(m, cfg=cfg, bandwidth=10.0)
+        assert enc.tobytes() == want, "encode n=%d ws=%d" % (n, ws)
+        dec, doff, dst = codec.decode_host(enc, eoff, max(n, 1))
+        assert int(dst[0]) == TDT_OK and int(doff[1]) == n and np.array_equal(dec, m), "decode n=%d" % n
+    # errors: short blob, bad magic, truncated TDT header
+    for bad, code in ((b"\x01\x02", 1), (b"ABCDEFGH", 2), (bytes.fromhex("44544454") + b"\x00" * 6, 3)):
+        b = np.frombuffer(bad, np.uint8)
+        dec, doff, dst = codec.decode_host(b, np.array([0, b.size], np.uint64), 64)
+        assert int(dst[0]) == code and int(doff[1]) == 0
+    assert codec.error_flags() == 0
+
+
+def test_encode_host_gather(orc):
+    """tdt_encode_host_v (the substrate send path: messages in separate caller buffers, gathered by
+    the copy pool straight into pinned staging) equals the oracle blob for blob, over a batch
+    large enough to be split into several 64 MiB pipeline chunks and gather pieces (small,
+    medium, 1 MiB and 3 MiB messages, odd sizes)."""
+    import ctypes as C
+    from psyne_amd._lib import check
+    rng = np.random.default_rng(97)
+    sizes = list(rng.integers(1, 2048, 3000) * 4) + [65536] * 600 + [1 << 20] * 60 + [3 << 20] * 4 + [1021, 0, 7]
+    rng.shuffle(sizes)
+    msgs = [np.ascontiguousarray(grad(rng, int(n) // 4).view(np.uint8)[: int(n)]) if n % 4 == 0 else
+            rng.integers(0, 256, int(n), dtype=np.uint8) for n in sizes]
+    n = len(msgs)
+    codec = make_codec()
+    ptrs = (C.c_void_p * n)(*[m.ctypes.data for m in msgs])
+    sz = np.array(sizes, np.uint64)
+    cap = int(sum(codec.encode_bound(int(s)) for s in sizes))
+    out = np.empty(cap, np.uint8)
+    ooff = np.zeros(n + 1, np.uint64)
+    st = np.zeros(n, np.int32)
+    check(codec._lib.tdt_encode_host_v(codec._h, C.addressof(ptrs), sz.ctypes.data, n, out.ctypes.data, cap,
+                                       ooff.ctypes.data, st.ctypes.data))
+    assert int(np.abs(st).sum()) == 0
+    for i, m in enumerate(msgs):
+        assert out[ooff[i]:ooff[i + 1]].tobytes() == orc.encode(m, bandwidth=10.0), "message %d (%d B)" % (i, m.size)
