@@ -26,8 +26,8 @@
 // The encode kernels live in tdt_enc_ws.hip (one translation unit per word size); diagnostic
 // builds (word size 4 only, phase profiling) instantiate them here instead.
 #if !defined(PSY_FAST_BUILD) && !(defined(PSY_PROF) && PSY_PROF) && !defined(PSY_SINGLE_TU)
-#define PSY_ENC_EXT(WS, T, G, M, L, TL, PS) \
-    extern template __global__ void psy::tdt_encode_kernel<WS, T, G, psy::M, L, TL, PS>(psy::EncodeArgs);
+#define PSY_ENC_EXT(WS, T, G, M, L, TL, PS, PA) \
+    extern template __global__ void psy::tdt_encode_kernel<WS, T, G, psy::M, L, TL, PS, PA>(psy::EncodeArgs);
 #define PSY_ENC_EXT_WS(WS)                 \
     PSY_ENC_INSTANCES(PSY_ENC_EXT, WS)     \
     extern template __global__ void psy::tdt_encode_lscan_kernel<WS>(psy::EncodeArgs, const uint32_t *, uint32_t);
@@ -468,7 +468,7 @@ int launch_slotted(tdt_ctx *c, PlanWS &pw, psy::EncodeArgs a, hipStream_t s) {
         reinterpret_cast<uint64_t *>(reinterpret_cast<uint8_t *>(trec) + sizeof(psy::TileRec) * pw.e_tcap);
     auto *shist = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(spans) + 8ull * (pw.e_tcap / psy::kSpanTiles));
     HIPCHK(hipMemsetAsync(cnt, 0, 128, s));
-    psy::PlanArgs p{a.in_off,  n,       cnt64,   slist,          mlist,              qlist,
+    psy::PlanArgs p{a.in,      a.in_off,  n,       cnt64,   slist,          mlist,              qlist,
                     blist,     clist,   tiles,   spans,          lmeta,              lcap,
                     tcap,      kSmallMax, kMidMax, kBigMin,      c->large_min,       small_on ? 1u : 0u,
                     mid_on ? 1u : 0u, a.min_tensor, (uint32_t)a.policy_on, (uint32_t)WS, copy_on ? 1u : 0u};
@@ -523,26 +523,45 @@ int launch_slotted(tdt_ctx *c, PlanWS &pw, psy::EncodeArgs a, hipStream_t s) {
         PSY_TILE_STEP(3, 6, tcap);  // emit
 #undef PSY_TILE_STEP
     }
-    // medium messages: one workgroup per list entry (the streaming-size ones first)
+    // medium messages: one workgroup per list entry — the big list first (longer or unaligned
+    // messages: the streaming-only kernel; a long team started last would run alone in the
+    // kernel's tail), then the medium list (resident-only kernel)
+    a.list2 = nullptr;
+    {
+        // (always launched: messages of a class switched off join it; the overflow launch ends at
+        // once when the list is empty)
+        a.list = blist;
+        a.list_count = cnt + 16;
+        both(H.valid ? (H.v[16] ? guess(H, 16, n, n) : 0u) : n, n, ovf512,
+             [&](uint32_t b, uint32_t g) {
+                 launch_list(g, 512, [&](uint32_t b2, uint32_t g2) {
+                     a.list_base = b + b2;
+                     hipLaunchKernelGGL((psy::tdt_encode_kernel<WS, 512, 8, MODE_ENCODE, 0, 0, 0, psy::PATH_STREAM>),
+                                        dim3(g2), dim3(512), 0, s, a);
+                 });
+             },
+             [&](uint32_t b, uint32_t g) {
+                 a.list_base = b;
+                 hipLaunchKernelGGL((psy::tdt_encode_kernel<WS, 512, 8, MODE_ENCODE, 0, 0, 1, psy::PATH_STREAM>), dim3(g),
+                                    dim3(512), 0, s, a);
+             });
+    }
     a.list = mlist;
     a.list_count = cnt + 2;
-    a.list2 = blist;
-    a.list2_count = cnt + 16;
-    const uint32_t gmed = H.valid ? std::min<uint32_t>(n, guess(H, 2, n, n) + guess(H, 16, n, n)) : n;
+    const uint32_t gmed = H.valid ? guess(H, 2, n, n) : n;
     both(gmed, n, ovf512,
          [&](uint32_t b, uint32_t g) {
              launch_list(g, 512, [&](uint32_t b2, uint32_t g2) {
                  a.list_base = b + b2;
-                 hipLaunchKernelGGL((psy::tdt_encode_kernel<WS, 512, 8, MODE_ENCODE, 0, 0, 0>), dim3(g2), dim3(512),
-                                    0, s, a);
+                 hipLaunchKernelGGL((psy::tdt_encode_kernel<WS, 512, 8, MODE_ENCODE, 0, 0, 0, psy::PATH_RES>), dim3(g2),
+                                    dim3(512), 0, s, a);
              });
          },
          [&](uint32_t b, uint32_t g) {
              a.list_base = b;
-             hipLaunchKernelGGL((psy::tdt_encode_kernel<WS, 512, 8, MODE_ENCODE, 0, 0, 1>), dim3(g), dim3(512), 0, s,
-                                a);
+             hipLaunchKernelGGL((psy::tdt_encode_kernel<WS, 512, 8, MODE_ENCODE, 0, 0, 1, psy::PATH_RES>), dim3(g),
+                                dim3(512), 0, s, a);
          });
-    a.list2 = nullptr;
     // small messages behind the tile pipeline on the side stream (the two streams' loads balance
     // better: C4's tile pipeline is shorter than its medium list)
     if (small_on) {
@@ -1295,8 +1314,12 @@ void launch_one_encode(const psy::EncodeArgs &a, uint64_t n, hipStream_t s) {
         hipLaunchKernelGGL((psy::tdt_encode_kernel<WS, 64, 4, MODE_ENCODE, 0, 0, 0>), dim3(1), dim3(64), 0, s, a);
     else if (n <= kMidMax)
         hipLaunchKernelGGL((psy::tdt_encode_kernel<WS, 256, 8, MODE_ENCODE, 0, 0, 0>), dim3(1), dim3(256), 0, s, a);
+    else if (n <= 65536 && (n & 15) == 0)  // (the block's input is 16-byte aligned: resident)
+        hipLaunchKernelGGL((psy::tdt_encode_kernel<WS, 512, 8, MODE_ENCODE, 0, 0, 0, psy::PATH_RES>), dim3(1),
+                           dim3(512), 0, s, a);
     else
-        hipLaunchKernelGGL((psy::tdt_encode_kernel<WS, 512, 8, MODE_ENCODE, 0, 0, 0>), dim3(1), dim3(512), 0, s, a);
+        hipLaunchKernelGGL((psy::tdt_encode_kernel<WS, 512, 8, MODE_ENCODE, 0, 0, 0, psy::PATH_STREAM>), dim3(1),
+                           dim3(512), 0, s, a);
 }
 
 // returns TDT_OK, an error, or -1: not taken (the pipeline serves the call)

@@ -10,7 +10,7 @@
 #error "PSY_INST_WS (the word size) must be defined"
 #endif
 
-#define PSY_ENC_DEF(WS, T, G, M, L, TL, PS) \
-    template __global__ void psy::tdt_encode_kernel<WS, T, G, psy::M, L, TL, PS>(psy::EncodeArgs);
+#define PSY_ENC_DEF(WS, T, G, M, L, TL, PS, PA) \
+    template __global__ void psy::tdt_encode_kernel<WS, T, G, psy::M, L, TL, PS, PA>(psy::EncodeArgs);
 PSY_ENC_INSTANCES(PSY_ENC_DEF, PSY_INST_WS)
 template __global__ void psy::tdt_encode_lscan_kernel<PSY_INST_WS>(psy::EncodeArgs, const uint32_t *, uint32_t);

@@ -97,7 +97,7 @@ struct EncodeArgs {
     int32_t *map_out;
     uint64_t *lookback;
     uint32_t *ticket;
-    uint32_t *errflags;  // bit0 look-back timeout, bit2 flush bound
+    uint32_t *errflags;  // bit0 look-back timeout, bit2 flush bound, bit3 a resident-only kernel got a streaming message
     const uint64_t *slot_off;  // slotted outputs (LB = 0): blob i at out + slot_off[i]
     uint64_t *out_len;         // slotted outputs: blob lengths
     uint64_t min_tensor;
@@ -182,8 +182,13 @@ enum {
     M_SB = 100 /*16*/, M_PART = 128 /*16 doubles: per-wave entropy partials*/, M_Z = 48 /*16: zero-bin totals*/,
     M_MAPBITS = 5 /*bit b = mapping[b]*/, M_READY = 6 /*deferred look-back: offset published*/
 };
-// decision margin of the mapping fast path, in bits of entropy (> 2x its worst-case error)
-constexpr double kFastMargin = 1e-4;
+// decision margin of the mapping fast path, in bits of entropy: > 2x its worst-case error
+// delta <= 2^-18 (hardware log2 per count) + 5·2^-24·log2 N (float sums of <= 4 bins, plus the
+// float count above 2^24) < 1.34e-5 for every N < 2^32.  (Was 1e-4 with 16-bin float groups: 0.7 % of C2's 1 KiB
+// uniform messages fell inside it and ran the exact fma chains, ~20k VALU each.)
+constexpr double kFastMargin = 3e-5;
+// bins summed per float group before the double accumulation
+constexpr int kFloatGroup = 4;
 
 // The slot layout of a byte-plane mapping (separate_byte_streams :527-549): slot j < L0 of a
 // 16-byte group is stream-0 byte j (word j / k0, position = the (j % k0)-th position mapped to
@@ -262,6 +267,19 @@ __device__ __forceinline__ const SlotLayout &slot_layout(uint32_t mb) {
     else if constexpr (WS == 4) return c_slots4.e[mb];
     else return c_slots8.e[mb];
 }
+// Speculated mapping of the fused count (DESIGN.md §4 "speculated count"): the byte-plane
+// mapping float gradients take (word size 4: the three low bytes high-entropy, the
+// sign/exponent byte low: mapping [1,1,1,0]; word size 8: [1,1,1,1,1,1,0,0]).  The histogram pass
+// of a streaming or tiled message also counts run starts under it; when the message's real
+// mapping turns out to be this one the count pass over the message is skipped (one read less).
+template <int WS>
+constexpr uint32_t spec_mapbits() {
+    return WS == 4 ? 0x7u : WS == 8 ? 0x3fu : 0xffffffffu;
+}
+// TileRec.clean written by the fused count when the tile may hold a 255-cap chunk start: the
+// count pass runs for that tile whatever the mapping
+constexpr uint32_t kRecount = 0xffffffffu;
+
 // per-wave slots (uint32, 8 per wave): 0,1 max(last run start+1); 2,3 chunk-start count;
 // 4 chunk bits of the wave's first group (combined slot layout)
 
@@ -301,7 +319,13 @@ __device__ __forceinline__ uint32_t spread2(uint32_t e) {
 // One message — or, TL > 0, part of a large message: TL 1 the histogram of one span of
 // kSpanTiles tiles (UNCP messages: the span's copy), 4 the mapping from the message's span
 // histograms (one team per message), 2 count and 3 emit one 64 KiB tile.
-template <int WS, int TEAM, int G, int MODE, int LB, int TL>
+// PATH: which bodies the instance holds — 0 both (resident and streaming), 1 resident only
+// (every message of its list is aligned and at most TEAM·G groups: the plan's medium list),
+// 2 streaming only (any message: the plan's big list).  Separate instances keep the streaming
+// body's live state out of the resident body's register allocation.
+enum { PATH_BOTH = 0, PATH_RES = 1, PATH_STREAM = 2 };
+
+template <int WS, int TEAM, int G, int MODE, int LB, int TL, int PATH = PATH_BOTH>
 __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, uint32_t msg, uint32_t lj,
                                            uint32_t tile) {
     static_assert(TL == 0 || (TEAM * G == (int)kTileGroups && MODE == MODE_ENCODE && !LB), "tile shape");
@@ -402,13 +426,24 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
         return;
     }
 
+    constexpr uint32_t kSpec = spec_mapbits<WS>();
+    // the histogram pass counts run starts under the speculated mapping: tiled messages (TL 1,
+    // one wave per tile) and streaming whole messages (TL 0)
+    constexpr bool SPECA1 = kSpec != 0xffffffffu && MODE == MODE_ENCODE && (TL == 0 || TL == 1);
+    if constexpr (TL == 2 && kSpec != 0xffffffffu) {
+        // the span pass counted this tile under the speculated mapping and it is the real one
+        const LMeta &lm = a.lmeta[lj];
+        if (lm.mapbits == kSpec && a.trec[lm.tile0 + tile].clean != kRecount) return;
+    }
+
     const uint32_t n32 = (uint32_t)n;
     const uint32_t wc = n32 / WS;
     const uint32_t ngroups = (n32 + 15) / 16;
     // the team's groups: the whole message, or one tile of it
     const uint32_t tg0 = TL ? tile * kTG : 0u;
     const uint32_t tgn = TL == 4 ? 0u : TL ? umin(ngroups - tg0, kTG) : ngroups;
-    const uint32_t RW = (tgn + TEAM - 1) / TEAM;  // rounds per wave
+    // rounds per wave; a span pass that counts gives every wave exactly one tile
+    const uint32_t RW = TL == 1 && SPECA1 ? kTileGroups / 64u : (tgn + TEAM - 1) / TEAM;
     const bool al16 = ((uintptr_t)base & 15) == 0;
     // Resident: the rounds fit in VGPRs and every group is a whole aligned 16 bytes, so the
     // loads are straight-line dwordx4s (below); anything else streams.
@@ -473,6 +508,7 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
                 if ((uint32_t)r < RW) body((uint32_t)r, dres[r], cres[r], std::true_type{});
         } else {
             for (uint32_t r = 0; r < RW; ++r) {
+                if (16ull * (gw0 + r * 64) >= n) break;  // (uniform) no group of the message left
                 uint4 d = load_group(gw0 + r * 64 + lane);
                 uint32_t c = 0;
                 body(r, d, c, std::false_type{});
@@ -483,6 +519,83 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
     // The message's mapping state: after the entropy terms wave 0 alone derives entropies,
     // mapping, slot layout and selectors (wave-local syncs), then ONE workgroup barrier.
     uint32_t *wm = reinterpret_cast<uint32_t *>(smem + Lay::OFF_WMISC);
+
+    // ---- speculated count (streaming / tiled messages): pass A1 below, restated on the
+    // speculated mapping's slot layout (a compile-time constant), run inside the histogram's
+    // rounds; the accumulators stand in for pass A1's when the real mapping is kSpec
+    constexpr bool SPEC_ON = SPECA1 && !RES;
+    constexpr SlotLayout SS = make_slot_layout<WS>(SPEC_ON ? kSpec : 0u);
+    constexpr bool s_ns2 = SS.ns == 2;
+    constexpr uint32_t s_L0 = SS.L0, s_Ls0 = SS.L0, s_Ls1 = s_ns2 ? 16u - SS.L0 : 0u;
+    constexpr uint32_t s_low = s_L0 >= 16 ? 0xffffu : ((1u << s_L0) - 1u);
+    constexpr bool s_fold = WS <= 4;
+    constexpr uint32_t s_p0sel =
+        s_fold && s_ns2 ? (0x06050400u & ~(0xffu << (2u * s_L0))) | (0x01u << (2u * s_L0)) : 0x06050400u;
+    constexpr uint64_t s_zk1[2] = {s_Ls0 < 16u ? 0x0101010101010101ull : 0x1111111111111111ull,
+                                   s_Ls1 < 16u ? 0x0101010101010101ull : 0x1111111111111111ull};
+    constexpr uint64_t s_zk8[2] = {s_Ls0 == 0u ? 0ull : s_Ls0 < 16u ? 0x8080808080808080ull : 0x8888888888888888ull,
+                                   s_Ls1 == 0u ? 0ull : s_Ls1 < 16u ? 0x8080808080808080ull : 0x8888888888888888ull};
+    uint32_t s_wmax[2] = {0, 0}, s_fmx[2] = {0, 0}, s_pc0 = 0, s_pc1 = 0, s_edc = 0;
+    uint64_t s_zacc = 0;
+    auto s_edges = [&](const uint4 &d) __attribute__((always_inline)) -> uint32_t {
+        return perm(d.y, d.x, SS.edA) | perm(d.w, d.z, SS.edB);
+    };
+    if constexpr (SPEC_ON) {
+        if (gw0 > 0 && gw0 - 1 < ngroups) s_edc = __builtin_amdgcn_readfirstlane(s_edges(load_group(gw0 - 1)));
+    }
+    auto spec_round = [&](uint32_t r, const uint4 &d) __attribute__((always_inline)) {
+        const uint32_t g = gw0 + r * 64 + lane;
+        uint32_t T[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) T[q] = perm(d.y, d.x, SS.selA[q]) | perm(d.w, d.z, SS.selB[q]);
+        const uint32_t ed = s_edges(d);
+        uint32_t V = 0xffffu;
+        if (!full_round(r)) {
+            const uint32_t nvw = vbytes(g) / WS;
+            if (nvw < (uint32_t)(16 / WS)) {
+                V = (1u << (nvw * SS.k0)) - 1u;
+                if (s_ns2) V |= ((1u << (nvw * SS.k1)) - 1u) << s_L0;
+            }
+        }
+        // run-start mask (the run_mask lambda of pass A1, on the constant layout)
+        const uint32_t pe = wave_shr1(ed, s_edc);
+        const uint32_t P0 = perm(T[3], pe, s_p0sel);
+        const uint32_t X[4] = {T[0] ^ P0, T[1] ^ T[0], T[2] ^ T[1], T[3] ^ T[2]};
+        uint32_t m = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t y = ((X[q] & 0x7f7f7f7fu) + 0x7f7f7f7fu) | X[q];
+            m |= (y >> (7 - q)) & (0x01010101u << q);
+        }
+        m = (m | (m >> 4)) & 0x00ff00ffu;
+        m = (m | (m >> 8)) & 0xffffu;
+        if constexpr (!s_fold && s_ns2) {
+            const uint32_t fx = ((ed >> 16) ^ (pe >> 8)) & 0xffu;
+            m = (m & ~(1u << s_L0)) | ((fx ? 1u : 0u) << s_L0);
+        }
+        if (r == 0u && gw0 == 0u && lane == 0) m |= 1u | (s_ns2 ? (1u << s_L0) : 0u);
+        m &= V;
+        s_edc = rdlane(ed, 63);
+        const uint64_t pastm = full_round(r) ? 0ull : (uint64_t)__ballot(g >= ngroups);
+        const uint32_t m0 = m & s_low;
+        if (m0) {
+            s_wmax[0] = umax(s_wmax[0], g * s_Ls0 + hibit(m0) + 1u);
+            if constexpr (TL == 1) s_fmx[0] = umax(s_fmx[0], ~(g * s_Ls0 + lobit(m0)));
+        }
+        s_pc0 += popc(m0);
+        const uint64_t b0 = (uint64_t)__ballot(m0 != 0u) | pastm;
+        s_zacc |= (b0 - s_zk1[0]) & ~b0 & s_zk8[0];
+        if constexpr (s_ns2) {
+            const uint32_t m1 = m >> s_L0;
+            if (m1) {
+                s_wmax[1] = umax(s_wmax[1], g * s_Ls1 + hibit(m1) + 1u);
+                if constexpr (TL == 1) s_fmx[1] = umax(s_fmx[1], ~(g * s_Ls1 + lobit(m1)));
+            }
+            s_pc1 += popc(m1);
+            const uint64_t b1 = (uint64_t)__ballot(m > s_low) | pastm;
+            s_zacc |= (b1 - s_zk1[1]) & ~b1 & s_zk8[1];
+        }
+    };
 
     // ------------------------------------------------------------ mapping (analysis)
     if constexpr (MODE == MODE_MAPPED || TL == 2 || TL == 3) {
@@ -575,9 +688,29 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
             PSY_ASM_ROUND(H);
             if (full_round(r)) hist_group(d, 16, true);
             else hist_group(d, vbytes(gw0 + r * 64 + lane), false);
+            if constexpr (SPEC_ON) spec_round(r, d);
         });
         team_sync<W>();
         PSY_PROF_MARK(1);
+        if constexpr (TL == 1 && SPEC_ON) {
+            // this wave's tile, counted under the speculated mapping (the count pass's record:
+            // last run start + 1, first run start, run starts, cap ruled out — or kRecount)
+            const LMeta &lm = a.lmeta[lj];
+            const uint32_t tl = tile * kSpanTiles + (uint32_t)wv;
+            const uint32_t w0 = wave_reduce<OpMax>(s_wmax[0]), w1 = wave_reduce<OpMax>(s_wmax[1]);
+            const uint32_t f0 = wave_reduce<OpMax>(s_fmx[0]), f1 = wave_reduce<OpMax>(s_fmx[1]);
+            const uint32_t p0 = wave_reduce<OpAdd>(s_pc0), p1 = wave_reduce<OpAdd>(s_pc1);
+            if (lane == 0 && tl < lm.ntiles) {
+                TileRec *t = a.trec + lm.tile0 + tl;
+                t->lrs[0] = w0;
+                t->lrs[1] = w1;
+                t->frs[0] = ~f0;
+                t->frs[1] = ~f1;
+                t->cnt[0] = p0;
+                t->cnt[1] = p1;
+                t->clean = s_zacc != 0ull ? kRecount : 1u;
+            }
+        }
         if constexpr (TL == 1) {
             // the span's histogram (its LDS copies and zero bins summed), for the map pass
             uint32_t *sh = a.shist + ((uint64_t)a.lmeta[lj].span0 + tile) * WS * 256;
@@ -606,7 +739,7 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
         // checked by tests/test_gpu_0_selftest.py).  The entropy calculate_entropy :470-480 computes
         // is e_b = log2 N - S_b/N up to the fma chain's rounding (< 5e-13), so a_b = log2 N - S_b/N
         // differs from it by delta < 2^-18 + 2^-23 + 1e-12, and mean(a) from the reference's mean by as
-        // much.  Whenever every |a_b - mean(a)| = |S_b - mean(S)| / N exceeds kFastMargin = 1e-4 (> 2·delta)
+        // much.  Whenever every |a_b - mean(a)| = |S_b - mean(S)| / N exceeds kFastMargin = 3e-5 (> 2·delta)
         // the mapping a_b > mean(a), i.e. S_b < mean(S), IS the reference's e_b > mean(e) (perform_clustering
         // :507-525).  Otherwise — ties: constant or repeated-distribution data — the exact fma chains in
         // bin order decide (below).  The sweep costs one log per bin and one reduction per position.
@@ -616,14 +749,16 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
             constexpr int BPT = TP >= 256 ? 1 : 256 / TP;
             const int pb = tid / TP, pj = tid % TP;
             // c·log2 c per bin in float (an empty bin: 0·log2 1 = 0), summed in float over groups of
-            // at most 16 bins and in double across groups: <= 17 roundings of 2^-24 relative each
-            // add at most 17·2^-24·log2 N < 3.3e-5 bits to the hardware log's 2^-18
+            // at most kFloatGroup bins and in double across groups: <= 5 roundings of 2^-24
+            // relative each on positive terms and partial sums (the float count above 2^24, the 4
+            // fmas of a group) add at most 5·2^-24·log2 N < 9.6e-6 bits to the hardware log's
+            // 2^-18
             double acc = 0.0;
 #pragma unroll
-            for (int k0 = 0; k0 < BPT; k0 += 16) {
+            for (int k0 = 0; k0 < BPT; k0 += kFloatGroup) {
                 float accf = 0.0f;
 #pragma unroll
-                for (int k = k0; k < (k0 + 16 < BPT ? k0 + 16 : BPT); ++k) {
+                for (int k = k0; k < (k0 + kFloatGroup < BPT ? k0 + kFloatGroup : BPT); ++k) {
                     const int v = pj + k * TP;
                     if (TP > 256 && v >= 256) break;  // (TEAM 512, word size 1: half the team idle)
                     const float cf = (float)count(pb, v);  // (0 for v = 0: the zero bins are summed below)
@@ -1066,7 +1201,18 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
         uint32_t fmx[2] = {0, 0};  // tile count pass: ~(first run start), max-reduced
         // stream position of this lane's group in round 0 (round r adds r·64·Ls)
         const uint32_t gL[2] = {(gw0 + (uint32_t)lane) * Ls[0], (gw0 + (uint32_t)lane) * Ls[1]};
-        {
+        bool spec_hit = false;
+        if constexpr (SPEC_ON && TL == 0) {
+            spec_hit = mapbits == kSpec;  // (uniform) the histogram pass counted under this mapping
+            if (spec_hit) {
+                wmax[0] = s_wmax[0];
+                wmax[1] = s_wmax[1];
+                pc0 = s_pc0;
+                pc1 = s_pc1;
+                zacc = s_zacc;
+            }
+        }
+        if (!spec_hit) {
             uint32_t edc = edc0;
             for_rounds([&](uint32_t r, uint4 &d, uint32_t &cm, auto res) __attribute__((always_inline)) {
                 PSY_ASM_ROUND(A1);
@@ -1739,8 +1885,21 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
         PSY_PROF_MARK(6);
     }
     };  // run
-    if (resident) run(std::true_type{});
-    else run(std::false_type{});
+    if constexpr (PATH == PATH_RES) {
+        if (resident) {
+            run(std::true_type{});
+        } else if (tid == 0) {
+            // (the plan never lists such a message here) flag it instead of a wild result
+            atomicOr(a.errflags, 8u);
+            if (a.status) a.status[msg] = ST_ARG;
+            if (a.out_len) a.out_len[msg] = 0;
+        }
+    } else if constexpr (PATH == PATH_STREAM) {
+        run(std::false_type{});
+    } else {
+        if (resident) run(std::true_type{});
+        else run(std::false_type{});
+    }
 }
 
 // Message ids: the compacted API's look-back needs them in dispatch order (atomic ticket);
@@ -1762,7 +1921,7 @@ __device__ __forceinline__ uint32_t entry_count(const EncodeArgs &a) {
     return __builtin_amdgcn_readfirstlane(c);
 }
 
-template <int WS, int TEAM, int G, int MODE, int LB, int TL = 0, int PS = 0>
+template <int WS, int TEAM, int G, int MODE, int LB, int TL = 0, int PS = 0, int PATH = PATH_BOTH>
 __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(EncodeArgs a) {
     using Lay = EncLayout<WS, TEAM>;
     constexpr int W = Lay::W;
@@ -1778,7 +1937,7 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
         const uint32_t n2 = TL == 0 && a.list2 ? __builtin_amdgcn_readfirstlane(*a.list2_count) : 0u;
         auto one = [&](uint32_t i) __attribute__((always_inline)) {
             if constexpr (TL == 0) {
-                encode_one<WS, TEAM, G, MODE, LB, 0>(a, smem, i < n2 ? a.list2[i] : a.list[i - n2], 0, 0);
+                encode_one<WS, TEAM, G, MODE, LB, 0, PATH>(a, smem, i < n2 ? a.list2[i] : a.list[i - n2], 0, 0);
             } else if constexpr (TL == 4) {
                 const uint32_t msg = a.lmeta[i].msg;  // one large message per workgroup
                 if (msg != kNone) encode_one<WS, TEAM, G, MODE, LB, TL>(a, smem, msg, i, 0);
@@ -1811,6 +1970,7 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
 // contiguous range of tile entries (tiles of one message in order); when the budgets (lmax
 // entries, tile_cap tiles) are spent it stays medium.
 struct PlanArgs {
+    const uint8_t *in;  // (alignment of each message: the medium list is resident-only)
     const uint64_t *in_off;
     uint32_t n_msgs;
     // [0] small (listed), [1] medium, [2] large entries, [3] tiles, [4] spans claimed, [5] small
@@ -1890,7 +2050,11 @@ __global__ __launch_bounds__(kPlanThreads) void tdt_encode_plan_kernel(PlanArgs 
         qc[k] = mid ? 1u : 0u;
         qm[k] = mid && p.mid_on ? 1u : 0u;
         const bool medium = valid && !large && !copy && !sm[k] && !qm[k];
-        bm[k] = medium && p.blist && n[k] > p.big_min ? 1u : 0u;
+        // the medium list's kernel holds only the resident body: longer or unaligned messages
+        // (and those of size not a multiple of 16) take the big list's streaming kernel
+        const bool res_ok = n[k] <= p.big_min && (n[k] & 15u) == 0 &&
+                            (((uintptr_t)p.in + (valid ? p.in_off[i] : 0ull)) & 15u) == 0;
+        bm[k] = medium && p.blist && !res_ok ? 1u : 0u;
         md[k] = medium && !bm[k] ? 1u : 0u;
     }
     wg_claim<kPlanPer>(sm, ps, p.cnt + 0, lds);
@@ -2004,13 +2168,14 @@ __global__ __launch_bounds__(64) void tdt_encode_lscan_kernel(EncodeArgs a, cons
 // The kernel instances of one word size.  The product library instantiates them in
 // tdt_enc_ws.hip, one translation unit per word size (compiled in parallel), and tdt_api.hip
 // declares them extern; diagnostic single-TU builds instantiate them implicitly.
-#define PSY_ENC_INSTANCES(X, WS)                                                                         \
-    X(WS, 512, 8, MODE_ENCODE, 0, 0, 0) X(WS, 512, 8, MODE_ENCODE, 0, 1, 0) X(WS, 512, 8, MODE_ENCODE, 0, 2, 0) \
-    X(WS, 512, 8, MODE_ENCODE, 0, 3, 0) X(WS, 512, 8, MODE_ENCODE, 0, 4, 0) X(WS, 64, 4, MODE_ENCODE, 0, 0, 0)  \
-    X(WS, 512, 8, MODE_ENCODE, 0, 0, 1) X(WS, 512, 8, MODE_ENCODE, 0, 1, 1) X(WS, 512, 8, MODE_ENCODE, 0, 2, 1) \
-    X(WS, 512, 8, MODE_ENCODE, 0, 3, 1) X(WS, 512, 8, MODE_ENCODE, 0, 4, 1) X(WS, 64, 4, MODE_ENCODE, 0, 0, 1)  \
-    X(WS, 256, 8, MODE_ENCODE, 0, 0, 0) X(WS, 256, 8, MODE_ENCODE, 0, 0, 1)                                     \
-    X(WS, 64, 4, MODE_ENCODE, 1, 0, 0) X(WS, 512, 8, MODE_ENCODE, 1, 0, 0) X(WS, 64, 4, MODE_MAPPED, 1, 0, 0)   \
-    X(WS, 512, 8, MODE_MAPPED, 1, 0, 0) X(WS, 64, 4, MODE_ANALYZE, 1, 0, 0) X(WS, 512, 8, MODE_ANALYZE, 1, 0, 0)
+#define PSY_ENC_INSTANCES(X, WS)                                                                                  \
+    X(WS, 512, 8, MODE_ENCODE, 0, 0, 0, 1) X(WS, 512, 8, MODE_ENCODE, 0, 0, 1, 1) X(WS, 512, 8, MODE_ENCODE, 0, 0, 0, 2) \
+    X(WS, 512, 8, MODE_ENCODE, 0, 0, 1, 2) X(WS, 512, 8, MODE_ENCODE, 0, 1, 0, 0) X(WS, 512, 8, MODE_ENCODE, 0, 2, 0, 0) \
+    X(WS, 512, 8, MODE_ENCODE, 0, 3, 0, 0) X(WS, 512, 8, MODE_ENCODE, 0, 4, 0, 0) X(WS, 64, 4, MODE_ENCODE, 0, 0, 0, 0)  \
+    X(WS, 512, 8, MODE_ENCODE, 0, 1, 1, 0) X(WS, 512, 8, MODE_ENCODE, 0, 2, 1, 0) X(WS, 512, 8, MODE_ENCODE, 0, 3, 1, 0) \
+    X(WS, 512, 8, MODE_ENCODE, 0, 4, 1, 0) X(WS, 64, 4, MODE_ENCODE, 0, 0, 1, 0) X(WS, 256, 8, MODE_ENCODE, 0, 0, 0, 0)  \
+    X(WS, 256, 8, MODE_ENCODE, 0, 0, 1, 0) X(WS, 64, 4, MODE_ENCODE, 1, 0, 0, 0) X(WS, 512, 8, MODE_ENCODE, 1, 0, 0, 0)  \
+    X(WS, 64, 4, MODE_MAPPED, 1, 0, 0, 0) X(WS, 512, 8, MODE_MAPPED, 1, 0, 0, 0) X(WS, 64, 4, MODE_ANALYZE, 1, 0, 0, 0)  \
+    X(WS, 512, 8, MODE_ANALYZE, 1, 0, 0, 0)
 
 }  // namespace psy
