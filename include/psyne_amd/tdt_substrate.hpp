@@ -837,7 +837,9 @@ private:
                 auto pick = [&]() -> RxBuf * {
                     for (auto &q : rx_pool_)
                         if (q->free) return q.get();
-                    if (rx_pool_.size() < kRxMax) {
+                    // read-ahead is kRing + 1 buffers; beyond that only what views hold (each
+                    // new buffer is a pinned allocation)
+                    if (rx_pool_.size() < std::min(kRxMax, kRing + 1 + rx_held_.size())) {
                         rx_pool_.push_back(std::make_unique<RxBuf>());
                         return rx_pool_.back().get();
                     }
