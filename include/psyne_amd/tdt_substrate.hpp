@@ -450,6 +450,20 @@ public:
     // keep a copy of each send_batch's blobs for last_batch() (tests; off by default)
     void record_last_batch(bool on) { record_last_ = on; }
 
+    // Where the pipeline's threads spent their time (seconds, cumulative; diagnostics).
+    struct PipeStats {
+        double encode = 0, tx_wait = 0;             // caller: encode calls / waiting for a tx buffer
+        double send = 0;                            // sender thread: socket writes
+        double recv = 0, rx_sleep = 0, rx_wait = 0; // receiver thread: filling / polling pauses / no free buffer
+        double decode = 0, dec_wait = 0;            // decoder thread: decode calls / idle
+        double deliver_wait = 0;                    // caller: waiting for decoded frames
+        uint64_t encode_calls = 0, decode_calls = 0, decode_bytes = 0;
+    };
+    PipeStats pipe_stats() {
+        std::lock_guard<std::mutex> a(tx_mu_), b(rx_mu_);
+        return st_;
+    }
+
     // Many messages per GPU call: the batch is encoded in sub-batches and queued for the sender
     // thread (one frame per blob, in order).  Returns the wire bytes of this batch.
     size_t send_batch(const void *const *data, const size_t *sizes, size_t n) {
@@ -472,7 +486,9 @@ public:
                 cap += tdt_encode_bound(sz[i + m], codec_.word_size());
                 ++m;
             }
+            auto t0 = Clock::now();
             TxBuf &b = tx_acquire();
+            auto t1 = Clock::now();
             b.mem.reserve(cap);
             b.off.assign(m + 1, 0);
             b.st.assign(m, 0);
@@ -487,6 +503,12 @@ public:
                     throw std::runtime_error(tdt_status_string(b.st[k]));
                 }
             b.n = m;
+            {
+                std::lock_guard<std::mutex> lk(tx_mu_);
+                st_.tx_wait += std::chrono::duration<double>(t1 - t0).count();
+                st_.encode += since(t1);
+                ++st_.encode_calls;
+            }
             if (record_last_) {
                 const uint64_t base = enc_.size();
                 enc_.insert(enc_.end(), b.mem.data(), b.mem.data() + b.off[m]);
@@ -660,6 +682,9 @@ private:
     static constexpr size_t kRxMax = 16;  // receive buffers at most (32 MiB of frames each)
     static constexpr uint64_t kRxEager = 4ull << 20;  // an idle decoder gets a buffer once it holds this much
 
+    using Clock = std::chrono::steady_clock;
+    static double since(Clock::time_point t) { return std::chrono::duration<double>(Clock::now() - t).count(); }
+
     // largest frame a <= payload-byte message can arrive as (TDT bound or UNCP n + 4)
     size_t frame_capacity(size_t payload) const { return tdt_encode_bound(payload, codec_.word_size()) + 64; }
 
@@ -717,6 +742,7 @@ private:
                 tx_queue_.erase(tx_queue_.begin());
                 tx_busy_ = true;
             }
+            auto t0 = Clock::now();
             try {
                 for (size_t k = 0; k < b->n; ++k)
                     inner_.transport_send(b->mem.data() + b->off[k], b->off[k + 1] - b->off[k]);
@@ -728,6 +754,7 @@ private:
             }
             {
                 std::lock_guard<std::mutex> lk(tx_mu_);
+                st_.send += since(t0);
                 b->free = true;
                 tx_busy_ = false;
             }
@@ -820,7 +847,9 @@ private:
     // the front buffer once decoded (waits); rethrows the pipeline's error when nothing is left
     RxBuf *wait_front() {
         std::unique_lock<std::mutex> lk(rx_mu_);
+        const auto t0 = Clock::now();
         rx_cv_.wait(lk, [&] { return rx_front_decoded() != nullptr || (rx_err_ && rx_drained()); });
+        st_.deliver_wait += since(t0);
         RxBuf *b = rx_front_decoded();
         if (!b) std::rethrow_exception(rx_err_);
         return b;
@@ -845,10 +874,12 @@ private:
                     }
                     return nullptr;
                 };
+                const auto tw = Clock::now();
                 rx_cv_.wait(lk, [&] {
                     if (rx_stop_ || rx_err_) return true;
                     return (b = pick()) != nullptr;
                 });
+                st_.rx_wait += since(tw);
                 if (rx_stop_ || rx_err_) return;
                 b->free = false;
                 b->sealed = b->decoded = false;
@@ -860,6 +891,8 @@ private:
             b->mem.reserve(std::max<uint64_t>(kRxBytes + fcap, 2 * fcap));
             auto pause = std::chrono::microseconds(1);
             auto last = std::chrono::steady_clock::now();
+            const auto tf = Clock::now();
+            double slept = 0;
             for (;;) {
                 size_t flen = 0;
                 bool got = false;
@@ -882,6 +915,8 @@ private:
                     const bool quiet = std::chrono::steady_clock::now() - last > std::chrono::microseconds(20);
                     if (full || (dec_idle_ && (b->off[b->n] >= kRxEager || quiet))) {
                         b->sealed = true;
+                        st_.recv += since(tf) - slept;
+                        st_.rx_sleep += slept;
                         break;
                     }
                 }
@@ -907,7 +942,9 @@ private:
                     rx_cv_.notify_all();
                     return;
                 }
+                const auto ts = Clock::now();
                 std::this_thread::sleep_for(pause);
+                slept += since(ts);
                 if (pause < std::chrono::microseconds(100)) pause *= 2;
             }
             rx_cv_.notify_all();
@@ -926,12 +963,15 @@ private:
                     return nullptr;
                 };
                 dec_idle_ = next() == nullptr;
+                const auto tw = Clock::now();
                 rx_cv_.wait(lk, [&] { return rx_stop_ || next() != nullptr; });
+                st_.dec_wait += since(tw);
                 dec_idle_ = false;
                 if (rx_stop_) return;
                 b = next();
                 lim = rx_max_msg_;
             }
+            const auto td = Clock::now();
             b->claim.resize(b->n);
             b->st.assign(b->n, TDT_OK);
             b->doff.assign(b->n + 1, 0);
@@ -974,6 +1014,9 @@ private:
             }
             {
                 std::lock_guard<std::mutex> lk(rx_mu_);
+                st_.decode += since(td);
+                ++st_.decode_calls;
+                st_.decode_bytes += b->off[b->n];
                 b->lim = lim;
                 b->decoded = true;
             }
@@ -987,6 +1030,7 @@ private:
     std::vector<uint8_t> stage_, enc_;
     std::vector<uint64_t> eoff_, dec_off_;
     size_t raw_sent_ = 0, wire_sent_ = 0, last_received_ = 0;
+    PipeStats st_;  // (tx fields under tx_mu_, rx fields under rx_mu_)
     bool record_last_ = false;
 
     std::mutex tx_mu_;

@@ -133,6 +133,9 @@ struct PlanWS {
     }
 };
 
+// host pipeline slots (chunks in flight per tdt_encode_host / tdt_decode_host call)
+constexpr int kHostSlots = 4;
+
 struct tdt_ctx {
     int device = 0;
     tdt_config cfg{};
@@ -155,7 +158,7 @@ struct tdt_ctx {
     uint8_t *h_dev = nullptr;
     size_t h_dev_bytes = 0;
     hipStream_t astream = nullptr;
-    // host pipeline (tdt_encode_host / tdt_decode_host): two slots, each with its own stream,
+    // host pipeline (tdt_encode_host / tdt_decode_host): kHostSlots slots, each with its own stream,
     // device buffer (input, offsets, output, status, look-back workspace) and pinned offsets
     struct HostSlot {
         hipStream_t stream = nullptr;
@@ -169,7 +172,7 @@ struct tdt_ctx {
         size_t sin_bytes = 0, sout_bytes = 0;
         hipEvent_t evc = nullptr;  // after the chunk's output copy (orders the next chunk's)
         PlanWS pw;
-    } hs[2];
+    } hs[kHostSlots];
     // one-message fast path (tdt_encode_host / tdt_decode_host with one message of at most
     // kOneMax bytes: the per-call Protocol::encode / decode of the drop-in class): a mapped pinned
     // block holding the call's offsets, list, status, input and output, read and written by ONE
@@ -931,9 +934,11 @@ size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 // ---------------------------------------------------------------------------------------
 // Host pipeline (the TCP socket-buffer case: SimpleTCP sends from and receives into host
 // memory, tcp_simple.hpp:68-91, :153-194).  The batch is cut into chunks of whole messages
-// (<= kHostChunk input bytes); chunk c runs on slot c % 2 — its own stream, device buffer,
-// look-back workspace and pinned buffers — as H2D → batch kernel → D2H, and the host finishes
-// chunk c - 1 (its output) while chunk c is on the GPU.  Caller buffers that are not pinned
+// (<= kHostChunk input bytes); chunk c runs on slot c % kHostSlots — its own stream, device
+// buffer, plan workspace and pinned buffers — as H2D → batch kernels → D2H, and the host finishes
+// chunk c - 3 (its output) while chunks c - 2 .. c are on the GPU: with two slots the next H2D
+// waited for the D2H of the chunk before (the pinned 50 x 1 MiB decode moved its bytes one PCIe
+// direction at a time: 22.6 GB/s, profiles/r04_hp1).  Caller buffers that are not pinned
 // (std::vector socket buffers, numpy arrays) are staged through the slot's pinned buffers by a
 // pool of host threads (parallel memcpy: one thread's memcpy is far below the PCIe rate);
 // pinned caller buffers are DMA'd directly.  Every device → host copy lands in pinned memory,
@@ -998,17 +1003,21 @@ int sync_slot(tdt_ctx *c, tdt_ctx::HostSlot &h) {
 struct Chunk {
     uint32_t m0 = 0, n = 0;
     uint64_t in_bytes = 0, cap = 0, base = 0;
-    size_t o_off = 0, o_out = 0, o_ooff = 0, o_st = 0, o_ws = 0;
+    uint64_t scap = 0;  // encode through the slotted kernels: the blobs' slot bytes (Σ bounds)
+    // device layout: input | in_off (n+1), slots (n+1) | out (cap) | out_off (n+1) | status (n)
+    // | workspace | lengths (n) | slotted blobs (scap)
+    size_t o_off = 0, o_out = 0, o_ooff = 0, o_st = 0, o_ws = 0, o_len = 0, o_sbuf = 0, end = 0;
 };
 
-// Chunk size of a call: a quarter of its input (so that H2D, kernel and D2H of neighbouring
-// chunks overlap even for a socket-sized batch of tens of MiB), between 4 and 64 MiB.
+// Chunk size of a call: an eighth of its input (with four slots in flight the H2D of later
+// chunks, the kernels of one and the D2H of earlier ones overlap even for a socket-sized batch
+// of tens of MiB), between 2 and 64 MiB.
 uint64_t host_chunk_bytes(const uint64_t *h_in_off, uint32_t n_msgs) {
     const uint64_t total = h_in_off[n_msgs] - h_in_off[0];
-    return std::min<uint64_t>(kHostChunk, std::max<uint64_t>(4ull << 20, (total / 4 + 4095) & ~4095ull));
+    return std::min<uint64_t>(kHostChunk, std::max<uint64_t>(2ull << 20, (total / 8 + 4095) & ~4095ull));
 }
 
-Chunk plan_chunk(const uint64_t *h_in_off, uint32_t m0, uint32_t n_msgs, bool encode, int ws,
+Chunk plan_chunk(const uint64_t *h_in_off, uint32_t m0, uint32_t n_msgs, bool encode, bool slotted, int ws,
                  const uint64_t *dec_sizes, uint64_t chunk_bytes) {
     Chunk k;
     k.m0 = m0;
@@ -1023,17 +1032,24 @@ Chunk plan_chunk(const uint64_t *h_in_off, uint32_t m0, uint32_t n_msgs, bool en
     k.n = m - m0;
     k.in_bytes = h_in_off[m] - h_in_off[m0];
     k.cap = cap;
+    k.scap = encode && slotted ? cap : 0;
     k.o_off = align_up(k.in_bytes, 256);
-    k.o_out = align_up(k.o_off + 8ull * (k.n + 1), 256);
+    k.o_out = align_up(k.o_off + 16ull * (k.n + 1), 256);
     k.o_ooff = align_up(k.o_out + std::max<uint64_t>(cap, 1), 256);
     k.o_st = align_up(k.o_ooff + 8ull * (k.n + 1), 256);
     k.o_ws = align_up(k.o_st + 4ull * k.n, 256);
+    k.o_len = align_up(k.o_ws + kCounterBytes + 8ull * (k.n + 1), 256);
+    k.o_sbuf = align_up(k.o_len + 8ull * k.n, 256);
+    k.end = k.o_sbuf + (k.scap ? k.scap + 16 : 0);  // (+16: the gather's funnel reads past a blob)
     return k;
 }
 
-size_t chunk_dev_bytes(const Chunk &k) { return k.o_ws + kCounterBytes + 8ull * (k.n + 1); }
-// pinned words of a slot: in_off (n+1) | out_off or slots (n+1) | lengths (n) | status (n int32)
-size_t chunk_pin_words(const Chunk &k) { return 3ull * k.n + 2 + (k.n + 1) / 2; }
+size_t chunk_dev_bytes(const Chunk &k) { return k.end; }
+// pinned words of a slot: in_off (n+1) | slots (n+1) | out_off or lengths (n+1) | status (n int32)
+size_t chunk_pin_words(const Chunk &k) { return 3ull * k.n + 3 + (k.n + 1) / 2; }
+uint64_t *pin_slots(tdt_ctx::HostSlot &h, const Chunk &k) { return h.pin + (k.n + 1); }
+uint64_t *pin_back(tdt_ctx::HostSlot &h, const Chunk &k) { return h.pin + 2ull * (k.n + 1); }
+int32_t *pin_status(tdt_ctx::HostSlot &h, const Chunk &k) { return reinterpret_cast<int32_t *>(h.pin + 3ull * k.n + 3); }
 
 // decode: the decoded size of every blob from its header (the kernel validates; a blob it
 // rejects gets 0 and its bytes are dropped when the output is compacted)
@@ -1046,6 +1062,31 @@ uint64_t host_decoded_size(const uint8_t *b, uint64_t len) {
     uint32_t orig;
     std::memcpy(&orig, b + 4, 4);
     return orig;
+}
+
+// One wave copies `len` bytes: 16-byte aligned stores; each 16-byte chunk read as five aligned
+// dwords and funnel-shifted by the (constant) source misalignment — compacted offsets have any
+// alignment, so a byte loop would be the common case otherwise.
+__device__ __forceinline__ void wave_copy_any(uint8_t *dst, const uint8_t *src, uint64_t len) {
+    const uint32_t lane = (uint32_t)psy::lane_id();
+    uint64_t head = (16 - ((uintptr_t)dst & 15)) & 15;
+    if (head > len) head = len;
+    if (lane < head) dst[lane] = src[lane];
+    const uint64_t nb = (len - head) / 16;
+    const uint8_t *s0 = src + head;
+    const uint32_t sh = (uint32_t)((uintptr_t)s0 & 3) * 8;
+    const uint32_t *sw = reinterpret_cast<const uint32_t *>((uintptr_t)s0 & ~(uintptr_t)3);
+    uint4 *dv = reinterpret_cast<uint4 *>(dst + head);
+    for (uint64_t k = lane; k < nb; k += 64) {
+        const uint32_t *q = sw + 4 * k;
+        const uint32_t w0 = psy::gload<uint32_t>(q), w1 = psy::gload<uint32_t>(q + 1), w2 = psy::gload<uint32_t>(q + 2),
+                       w3 = psy::gload<uint32_t>(q + 3);
+        // (the fifth dword only when misaligned: it may lie past the source's end otherwise)
+        const uint32_t w4 = sh ? psy::gload<uint32_t>(q + 4) : 0u;
+        dv[k] = make_uint4((uint32_t)((((uint64_t)w1 << 32) | w0) >> sh), (uint32_t)((((uint64_t)w2 << 32) | w1) >> sh),
+                           (uint32_t)((((uint64_t)w3 << 32) | w2) >> sh), (uint32_t)((((uint64_t)w4 << 32) | w3) >> sh));
+    }
+    for (uint64_t k = head + 16 * nb + lane; k < len; k += 64) dst[k] = src[k];
 }
 
 // Chunk ci's compacted output → host memory, issued behind the encode kernel so that no host
@@ -1082,6 +1123,83 @@ __global__ __launch_bounds__(256) void host_out_kernel(const uint8_t *src, const
     for (uint64_t k = head + 16 * nb + gtid; k < total; k += gsz) d[k] = src[k];
 }
 
+// A slotted chunk's blob lengths → exclusive offsets (total at [n]): one workgroup, 4096
+// lengths per step (a chunk holds at most kHostChunk bytes of messages).
+__global__ __launch_bounds__(1024) void host_scan_kernel(const uint64_t *len, uint64_t *out_off, uint32_t n) {
+    __shared__ uint64_t wsum[16];
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    uint64_t carry = 0;
+    for (uint32_t b = 0; b < n; b += 4096) {
+        uint64_t v[4], s = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t i = b + 4u * (uint32_t)t + (uint32_t)k;
+            v[k] = i < n ? len[i] : 0ull;
+            s += v[k];
+        }
+        uint64_t x = s;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint64_t y = __shfl_up(x, d);
+            if (lane >= d) x += y;
+        }
+        if (lane == 63) wsum[wv] = x;
+        __syncthreads();
+        uint64_t pre = carry, tot = 0;
+#pragma unroll
+        for (int w = 0; w < 16; ++w) {
+            const uint64_t q = wsum[w];
+            pre += w < wv ? q : 0ull;
+            tot += q;
+        }
+        uint64_t e = pre + x - s;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t i = b + 4u * (uint32_t)t + (uint32_t)k;
+            if (i < n) out_off[i] = e;
+            e += v[k];
+        }
+        carry += tot;
+        __syncthreads();  // wsum is reused
+    }
+    if (t == 0) out_off[n] = carry;
+}
+
+// A slotted chunk's blobs → host memory at their compacted places (the output copy of
+// host_out_kernel, gathering from the slots): P waves per blob, each a contiguous part; the
+// running base is chained as there.
+__global__ __launch_bounds__(256) void host_gather_kernel(const uint8_t *src, const uint64_t *slot, const uint64_t *len,
+                                                          const uint64_t *out_off, uint32_t n, uint32_t P, uint8_t *dst,
+                                                          uint64_t *bases, uint32_t ci, uint64_t cap, int direct) {
+    const uint64_t total = out_off[n];
+    const uint64_t base = bases[ci];
+    if (blockIdx.x == 0 && threadIdx.x == 0) bases[ci + 1] = base + total;
+    if (base + total > cap || total == 0) return;
+    uint8_t *d = direct ? dst + base : dst;
+    const uint64_t nw = (uint64_t)n * P;
+    for (uint64_t w = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); w < nw; w += (uint64_t)gridDim.x * 4) {
+        const uint32_t i = (uint32_t)(w / P), p = (uint32_t)(w % P);
+        const uint64_t l = len[i], a = l * p / P, e = l * (p + 1) / P;
+        if (e > a) wave_copy_any(d + out_off[i] + a, src + slot[i] + a, e - a);
+    }
+}
+
+// The issue / finish loop of a host call: chunk ci is issued on slot ci % kHostSlots once that
+// slot's previous chunk is done, and finished (its outputs and statuses read back) kHostSlots - 1
+// chunks later, so that up to kHostSlots chunks are in flight.
+template <class I, class F>
+int host_loop(size_t nc, I &&issue, F &&finish) {
+    constexpr size_t L = kHostSlots - 1;
+    for (size_t ci = 0; ci < nc; ++ci) {
+        int st = issue(ci);
+        if (!st && ci >= L) st = finish(ci - L);
+        if (st) return st;
+    }
+    for (size_t ci = nc > L ? nc - L : 0; ci < nc; ++ci)
+        if (int st = finish(ci)) return st;
+    return TDT_OK;
+}
+
 // msgs / sizes (gather input, tdt_encode_host_v): message i = msgs[i][0 .. sizes[i]); h_in is then
 // unused and h_in_off holds the prefix sums of sizes
 int host_encode(tdt_ctx *c, const uint8_t *h_in, const uint64_t *h_in_off, uint32_t n_msgs, uint8_t *h_out,
@@ -1096,10 +1214,15 @@ int host_encode(tdt_ctx *c, const uint8_t *h_in, const uint64_t *h_in_off, uint3
         d_out = nullptr;
     }
     const bool pin_out = d_out != nullptr;
+    // one pass with the look-back when every message is <= 64 KiB and they average >= 16 KiB (as
+    // tdt_encode_batch); otherwise the slotted message-class kernels (a 1 MiB message spreads over
+    // 64 KiB tiles instead of running in one workgroup) and a gather into the host buffer
+    bool lb = h_in_off[n_msgs] - h_in_off[0] >= 16384ull * n_msgs;
+    for (uint32_t i = 0; i < n_msgs && lb; ++i) lb = h_in_off[i + 1] - h_in_off[i] <= kBigMin;
     std::vector<Chunk> ch;
     const uint64_t cb = host_chunk_bytes(h_in_off, n_msgs);
     for (uint32_t m = 0; m < n_msgs;) {
-        ch.push_back(plan_chunk(h_in_off, m, n_msgs, true, ws, nullptr, cb));
+        ch.push_back(plan_chunk(h_in_off, m, n_msgs, true, !lb, ws, nullptr, cb));
         m += ch.back().n;
     }
     if (ch.size() + 1 > c->hbases_n) {
@@ -1112,15 +1235,22 @@ int host_encode(tdt_ctx *c, const uint8_t *h_in, const uint64_t *h_in_off, uint3
     bool capacity = false;
     auto issue = [&](size_t ci) -> int {
         const Chunk &k = ch[ci];
-        auto &h = c->hs[ci & 1];
-        int st = ensure_slot(c, (int)(ci & 1), chunk_dev_bytes(k), chunk_pin_words(k), pin_in ? 0 : k.in_bytes,
-                             pin_out ? 0 : k.cap);
+        const int si = (int)(ci % kHostSlots);
+        auto &h = c->hs[si];
+        int st = ensure_slot(c, si, chunk_dev_bytes(k), chunk_pin_words(k), pin_in ? 0 : k.in_bytes, pin_out ? 0 : k.cap);
         if (st) return st;
         st = sync_slot(c, h);  // the slot's previous chunk is done with its buffers
         if (st) return st;
-        uint64_t *pin_in_off = h.pin;
+        uint64_t *pin_in_off = h.pin, *pin_slot = pin_slots(h, k);
         const uint64_t b0 = h_in_off[k.m0];
-        for (uint32_t i = 0; i <= k.n; ++i) pin_in_off[i] = h_in_off[k.m0 + i] - b0;
+        uint64_t acc = 0;
+        for (uint32_t i = 0; i <= k.n; ++i) {
+            pin_in_off[i] = h_in_off[k.m0 + i] - b0;
+            if (k.scap) {
+                pin_slot[i] = acc;
+                if (i < k.n) acc += tdt_encode_bound(h_in_off[k.m0 + i + 1] - h_in_off[k.m0 + i], ws);
+            }
+        }
         const uint8_t *src = msgs ? nullptr : h_in + b0;
         if (msgs) {
             c->pool->gather(h.stage_in, msgs + k.m0, sizes + k.m0, k.n);
@@ -1131,49 +1261,63 @@ int host_encode(tdt_ctx *c, const uint8_t *h_in, const uint64_t *h_in_off, uint3
         }
         uint8_t *d = h.dev;
         auto *doff = reinterpret_cast<uint64_t *>(d + k.o_off);
+        auto *dslot = doff + (k.n + 1);
         auto *dooff = reinterpret_cast<uint64_t *>(d + k.o_ooff);
         auto *dst = reinterpret_cast<int32_t *>(d + k.o_st);
+        auto *dlen = reinterpret_cast<uint64_t *>(d + k.o_len);
         HIPCHK(hipMemcpyAsync(d, src, k.in_bytes, hipMemcpyHostToDevice, h.stream));
-        HIPCHK(hipMemcpyAsync(doff, pin_in_off, 8ull * (k.n + 1), hipMemcpyHostToDevice, h.stream));
-        st = encode_common(c, psy::MODE_ENCODE, d, doff, k.n, nullptr, d + k.o_out, k.cap, dooff, dst, nullptr, nullptr,
-                           nullptr, h.stream, nullptr, nullptr, d + k.o_ws, nullptr,
-                           k.in_bytes <= kSmallMax * k.n ? 1 : 0);  // (the chunk's sizes are host data)
-        if (st) return st;
+        // in_off and (slotted) the slots: one copy
+        HIPCHK(hipMemcpyAsync(doff, pin_in_off, (k.scap ? 16ull : 8ull) * (k.n + 1), hipMemcpyHostToDevice, h.stream));
+        if (k.scap) {
+            st = encode_common(c, psy::MODE_ENCODE, d, doff, k.n, nullptr, d + k.o_sbuf, k.scap, nullptr, dst, nullptr,
+                               nullptr, nullptr, h.stream, dslot, dlen, d + k.o_ws, &h.pw);
+            if (st) return st;
+            hipLaunchKernelGGL(host_scan_kernel, dim3(1), dim3(1024), 0, h.stream, dlen, dooff, k.n);
+            HIPCHK(hipGetLastError());
+        } else {
+            st = encode_common(c, psy::MODE_ENCODE, d, doff, k.n, nullptr, d + k.o_out, k.cap, dooff, dst, nullptr,
+                               nullptr, nullptr, h.stream, nullptr, nullptr, d + k.o_ws, nullptr,
+                               k.in_bytes <= kSmallMax * k.n ? 1 : 0);  // (the chunk's sizes are host data)
+            if (st) return st;
+        }
         // the output, in chunk order (each copy follows the previous chunk's: the running base)
         if (ci == 0) HIPCHK(hipMemsetAsync(c->hbases, 0, 8, h.stream));
-        else HIPCHK(hipStreamWaitEvent(h.stream, c->hs[(ci - 1) & 1].evc, 0));
-        const uint32_t grid = (uint32_t)std::min<uint64_t>(1024, k.cap / 4096 + 1);
-        hipLaunchKernelGGL(host_out_kernel, dim3(grid), dim3(256), 0, h.stream, d + k.o_out, dooff, k.n,
-                           pin_out ? d_out : h.stage_out, c->hbases, (uint32_t)ci, out_cap, pin_out ? 1 : 0);
+        else HIPCHK(hipStreamWaitEvent(h.stream, c->hs[(ci - 1) % kHostSlots].evc, 0));
+        uint8_t *odst = pin_out ? d_out : h.stage_out;
+        if (k.scap) {
+            const uint32_t P = (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(1, k.in_bytes / k.n / 16384));
+            const uint32_t grid = (uint32_t)std::min<uint64_t>(2048, ((uint64_t)k.n * P + 3) / 4);
+            hipLaunchKernelGGL(host_gather_kernel, dim3(grid), dim3(256), 0, h.stream, d + k.o_sbuf, dslot, dlen, dooff,
+                               k.n, P, odst, c->hbases, (uint32_t)ci, out_cap, pin_out ? 1 : 0);
+        } else {
+            const uint32_t grid = (uint32_t)std::min<uint64_t>(1024, k.cap / 4096 + 1);
+            hipLaunchKernelGGL(host_out_kernel, dim3(grid), dim3(256), 0, h.stream, d + k.o_out, dooff, k.n, odst,
+                               c->hbases, (uint32_t)ci, out_cap, pin_out ? 1 : 0);
+        }
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(h.evc, h.stream));
         HIPCHK(hipMemcpyAsync(h.flag, d + k.o_ws + 4, 4, hipMemcpyDeviceToHost, h.stream));
-        HIPCHK(hipMemcpyAsync(h.pin + (k.n + 1), dooff, 8ull * (k.n + 1), hipMemcpyDeviceToHost, h.stream));
-        HIPCHK(hipMemcpyAsync(h.pin + 3ull * k.n + 2, dst, 4ull * k.n, hipMemcpyDeviceToHost, h.stream));
+        HIPCHK(hipMemcpyAsync(pin_back(h, k), dooff, 8ull * (k.n + 1), hipMemcpyDeviceToHost, h.stream));
+        HIPCHK(hipMemcpyAsync(pin_status(h, k), dst, 4ull * k.n, hipMemcpyDeviceToHost, h.stream));
         HIPCHK(hipEventRecord(h.ev, h.stream));
         return TDT_OK;
     };
     // chunk ci's compacted size is known once its event fires; then its output comes back
     auto finish = [&](size_t ci) -> int {
         const Chunk &k = ch[ci];
-        auto &h = c->hs[ci & 1];
+        auto &h = c->hs[ci % kHostSlots];
         HIPCHK(hipEventSynchronize(h.ev));
-        const uint64_t *pin_out_off = h.pin + (k.n + 1);
+        const uint64_t *pin_out_off = pin_back(h, k);
         const uint64_t total = pin_out_off[k.n];
         if (capacity || base + total > out_cap) capacity = true;
         for (uint32_t i = 0; i < k.n; ++i) h_out_off[k.m0 + i] = base + (capacity ? 0 : pin_out_off[i]);
-        if (h_status) std::memcpy(h_status + k.m0, h.pin + 3ull * k.n + 2, 4ull * k.n);
+        if (h_status) std::memcpy(h_status + k.m0, pin_status(h, k), 4ull * k.n);
         // (the copy kernel has written the output: into h_out directly, or into the staging)
         if (!capacity && total && !pin_out) c->pool->copy(h_out + base, h.stage_out, total);
         if (!capacity) base += total;
         return TDT_OK;
     };
-    for (size_t ci = 0; ci < ch.size(); ++ci) {
-        int st = issue(ci);
-        if (!st && ci > 0) st = finish(ci - 1);
-        if (st) return st;
-    }
-    int st = finish(ch.size() - 1);
+    int st = host_loop(ch.size(), issue, finish);
     if (st) return st;
     for (auto &h : c->hs)
         if (h.stream && (st = sync_slot(c, h))) return st;
@@ -1198,7 +1342,7 @@ int host_decode(tdt_ctx *c, const uint8_t *h_in, const uint64_t *h_in_off, uint3
     uint64_t base = 0;
     const uint64_t cb = host_chunk_bytes(h_in_off, n_msgs);
     for (uint32_t m = 0; m < n_msgs;) {
-        ch.push_back(plan_chunk(h_in_off, m, n_msgs, false, c->cfg.word_size, dsz.data(), cb));
+        ch.push_back(plan_chunk(h_in_off, m, n_msgs, false, false, c->cfg.word_size, dsz.data(), cb));
         ch.back().base = base;
         base += ch.back().cap;
         m += ch.back().n;
@@ -1207,13 +1351,13 @@ int host_decode(tdt_ctx *c, const uint8_t *h_in, const uint64_t *h_in_off, uint3
     std::vector<int32_t> stv(n_msgs);
     auto issue = [&](size_t ci) -> int {
         const Chunk &k = ch[ci];
-        auto &h = c->hs[ci & 1];
-        int st = ensure_slot(c, (int)(ci & 1), chunk_dev_bytes(k) + 8ull * k.n, chunk_pin_words(k),
-                             pin_in ? 0 : k.in_bytes, pin_out ? 0 : k.cap);
+        const int si = (int)(ci % kHostSlots);
+        auto &h = c->hs[si];
+        int st = ensure_slot(c, si, chunk_dev_bytes(k), chunk_pin_words(k), pin_in ? 0 : k.in_bytes, pin_out ? 0 : k.cap);
         if (st) return st;
         st = sync_slot(c, h);
         if (st) return st;
-        uint64_t *pin_in_off = h.pin, *pin_slot = h.pin + (k.n + 1);
+        uint64_t *pin_in_off = h.pin, *pin_slot = pin_slots(h, k);
         const uint64_t b0 = h_in_off[k.m0];
         uint64_t acc = 0;
         for (uint32_t i = 0; i <= k.n; ++i) {
@@ -1228,12 +1372,11 @@ int host_decode(tdt_ctx *c, const uint8_t *h_in, const uint64_t *h_in_off, uint3
         }
         uint8_t *d = h.dev;
         auto *doff = reinterpret_cast<uint64_t *>(d + k.o_off);
-        auto *dslot = reinterpret_cast<uint64_t *>(d + k.o_ooff);
+        auto *dslot = doff + (k.n + 1);
         auto *dst = reinterpret_cast<int32_t *>(d + k.o_st);
-        auto *dlen = reinterpret_cast<uint64_t *>(d + chunk_dev_bytes(k));
+        auto *dlen = reinterpret_cast<uint64_t *>(d + k.o_len);
         HIPCHK(hipMemcpyAsync(d, src, k.in_bytes, hipMemcpyHostToDevice, h.stream));
-        HIPCHK(hipMemcpyAsync(doff, pin_in_off, 8ull * (k.n + 1), hipMemcpyHostToDevice, h.stream));
-        HIPCHK(hipMemcpyAsync(dslot, pin_slot, 8ull * (k.n + 1), hipMemcpyHostToDevice, h.stream));
+        HIPCHK(hipMemcpyAsync(doff, pin_in_off, 16ull * (k.n + 1), hipMemcpyHostToDevice, h.stream));  // offsets + slots
         st = decode_common(c, false, d, doff, k.n, d + k.o_out, 0, nullptr, nullptr, dst, h.stream, dslot, dlen,
                            nullptr, d + k.o_ws, &h.pw);
         if (st) return st;
@@ -1241,26 +1384,21 @@ int host_decode(tdt_ctx *c, const uint8_t *h_in, const uint64_t *h_in_off, uint3
         if (acc)
             HIPCHK(hipMemcpyAsync(pin_out ? h_out + k.base : h.stage_out, d + k.o_out, acc, hipMemcpyDeviceToHost,
                                   h.stream));
-        HIPCHK(hipMemcpyAsync(h.pin + 2ull * (k.n + 1), dlen, 8ull * k.n, hipMemcpyDeviceToHost, h.stream));
-        HIPCHK(hipMemcpyAsync(h.pin + 3ull * k.n + 2, dst, 4ull * k.n, hipMemcpyDeviceToHost, h.stream));
+        HIPCHK(hipMemcpyAsync(pin_back(h, k), dlen, 8ull * k.n, hipMemcpyDeviceToHost, h.stream));
+        HIPCHK(hipMemcpyAsync(pin_status(h, k), dst, 4ull * k.n, hipMemcpyDeviceToHost, h.stream));
         HIPCHK(hipEventRecord(h.ev, h.stream));
         return TDT_OK;
     };
     auto finish = [&](size_t ci) -> int {
         const Chunk &k = ch[ci];
-        auto &h = c->hs[ci & 1];
+        auto &h = c->hs[ci % kHostSlots];
         HIPCHK(hipEventSynchronize(h.ev));
         if (!pin_out && k.cap) c->pool->copy(h_out + k.base, h.stage_out, k.cap);
-        std::memcpy(lens.data() + k.m0, h.pin + 2ull * (k.n + 1), 8ull * k.n);
-        std::memcpy(stv.data() + k.m0, h.pin + 3ull * k.n + 2, 4ull * k.n);
+        std::memcpy(lens.data() + k.m0, pin_back(h, k), 8ull * k.n);
+        std::memcpy(stv.data() + k.m0, pin_status(h, k), 4ull * k.n);
         return TDT_OK;
     };
-    for (size_t ci = 0; ci < ch.size(); ++ci) {
-        int st = issue(ci);
-        if (!st && ci > 0) st = finish(ci - 1);
-        if (st) return st;
-    }
-    int st = finish(ch.size() - 1);
+    int st = host_loop(ch.size(), issue, finish);
     if (st) return st;
     for (auto &h : c->hs) {
         st = h.stream ? sync_slot(c, h) : TDT_OK;
@@ -1465,31 +1603,6 @@ __global__ __launch_bounds__(256) void cp_len_kernel(const uint64_t *len, uint64
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
     if (i < n) out_off[i] = len[i];
 }
-// One wave copies one blob: 16-byte aligned stores; each 16-byte chunk read as five aligned
-// dwords and funnel-shifted by the (constant) source misalignment — compacted offsets have any
-// alignment, so a byte loop would be the common case otherwise.
-__device__ __forceinline__ void wave_copy_any(uint8_t *dst, const uint8_t *src, uint64_t len) {
-    const uint32_t lane = (uint32_t)psy::lane_id();
-    uint64_t head = (16 - ((uintptr_t)dst & 15)) & 15;
-    if (head > len) head = len;
-    if (lane < head) dst[lane] = src[lane];
-    const uint64_t nb = (len - head) / 16;
-    const uint8_t *s0 = src + head;
-    const uint32_t sh = (uint32_t)((uintptr_t)s0 & 3) * 8;
-    const uint32_t *sw = reinterpret_cast<const uint32_t *>((uintptr_t)s0 & ~(uintptr_t)3);
-    uint4 *dv = reinterpret_cast<uint4 *>(dst + head);
-    for (uint64_t k = lane; k < nb; k += 64) {
-        const uint32_t *q = sw + 4 * k;
-        const uint32_t w0 = psy::gload<uint32_t>(q), w1 = psy::gload<uint32_t>(q + 1), w2 = psy::gload<uint32_t>(q + 2),
-                       w3 = psy::gload<uint32_t>(q + 3);
-        // (the fifth dword only when misaligned: it may lie past the source's end otherwise)
-        const uint32_t w4 = sh ? psy::gload<uint32_t>(q + 4) : 0u;
-        dv[k] = make_uint4((uint32_t)((((uint64_t)w1 << 32) | w0) >> sh), (uint32_t)((((uint64_t)w2 << 32) | w1) >> sh),
-                           (uint32_t)((((uint64_t)w3 << 32) | w2) >> sh), (uint32_t)((((uint64_t)w4 << 32) | w3) >> sh));
-    }
-    for (uint64_t k = head + 16 * nb + lane; k < len; k += 64) dst[k] = src[k];
-}
-
 // blob i (one wave each, four per workgroup): slot → its compacted place (capacity: the
 // TDT_E_CAPACITY of the look-back path; out_off keeps the full prefix sum either way)
 __global__ __launch_bounds__(256) void cp_gather_kernel(const uint8_t *src, const uint64_t *slot, const uint64_t *len,

@@ -1112,7 +1112,7 @@ struct DPlanArgs {
 };
 
 __global__ __launch_bounds__(1024) void tdt_decode_plan_kernel(DPlanArgs p) {
-    __shared__ uint64_t lds[4 * 16 + 1];
+    __shared__ uint64_t lds[6 * (4 * 16 + 1)];
     // one wave per blob keeps the chip busy while a blob is at most ~1/4096 of the batch's
     // bytes; only larger blobs (and only above large_min) are worth the tiled passes
     uint64_t thr = p.large_min;
@@ -1121,8 +1121,13 @@ __global__ __launch_bounds__(1024) void tdt_decode_plan_kernel(DPlanArgs p) {
         const uint64_t share = (last - p.in_off[0]) / 4096;
         thr = share > thr ? share : thr;
     }
-    uint64_t isl[4], nt[4], nb[4], j[4], t0[4], b0[4], one[4], pos[4], sm[4], spos[4], sc[4], scp[4], bg[4], bpos[4];
-    uint64_t osz_k[4], unc[4] = {0, 0, 0, 0}, cpo[4], cpp[4], ucc[4], ucp[4];
+    // the claims' values (A: large blobs, tiles, block slots; B: the lists) and their starts
+    uint64_t A[3][4], SA[3][4], B[6][4], SB[6][4];
+    auto &isl = A[0], &nt = A[1], &nb = A[2];
+    auto &j = SA[0], &t0 = SA[1], &b0 = SA[2];
+    auto &one = B[0], &sm = B[1], &sc = B[2], &bg = B[3], &ucc = B[4], &cpo = B[5];
+    auto &pos = SB[0], &spos = SB[1], &bpos = SB[3], &cpp = SB[5];
+    uint64_t osz_k[4], unc[4] = {0, 0, 0, 0};
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const uint32_t i = (blockIdx.x * 4 + k) * 1024 + threadIdx.x;
@@ -1153,9 +1158,10 @@ __global__ __launch_bounds__(1024) void tdt_decode_plan_kernel(DPlanArgs p) {
             }
         }
     }
-    wg_claim<4>(isl, j, p.cnt + 1, lds);
-    wg_claim<4>(nt, t0, p.cnt + 2, lds);
-    wg_claim<4>(nb, b0, p.cnt + 3, lds);
+    {
+        constexpr int ia[3] = {1, 2, 3};
+        wg_claim_n<3, 4>(A, SA, p.cnt, ia, lds);
+    }
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const uint32_t i = (blockIdx.x * 4 + k) * 1024 + threadIdx.x;
@@ -1188,12 +1194,10 @@ __global__ __launch_bounds__(1024) void tdt_decode_plan_kernel(DPlanArgs p) {
         bg[k] = big ? 1u : 0u;
         one[k] = (any && !sm[k] && !big) ? 1u : 0u;
     }
-    wg_claim<4>(one, pos, p.cnt, lds);
-    wg_claim<4>(sm, spos, p.cnt + 4, lds);
-    wg_claim<4>(sc, scp, p.cnt + 5, lds);
-    wg_claim<4>(bg, bpos, p.cnt + 6, lds);
-    wg_claim<4>(ucc, ucp, p.cnt + 7, lds);
-    wg_claim<4>(cpo, cpp, p.cnt + 8, lds);
+    {
+        constexpr int ib[6] = {0, 4, 5, 6, 7, 8};
+        wg_claim_n<6, 4>(B, SB, p.cnt, ib, lds);
+    }
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         if (one[k]) p.list[pos[k]] = (blockIdx.x * 4 + k) * 1024 + threadIdx.x;

@@ -267,18 +267,78 @@ __device__ __forceinline__ void wg_claim(const uint64_t (&v)[NK], uint64_t (&sta
         if (lane == 63) lds[k * 16 + wv] = x;
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        uint64_t t = 0;
-        for (int e = 0; e < NK * 16; ++e) {
-            const uint64_t x = lds[e];
-            lds[e] = t;
-            t += x;
+    // the NK·16 wave totals scanned by wave 0, one per lane (a serial loop over them by one
+    // thread was ~3 µs of LDS round trips per call: most of a one-workgroup plan's time)
+    static_assert(NK * 16 <= 64, "one wave scans the wave totals");
+    if (wv == 0) {
+        const uint64_t x = lane < NK * 16 ? lds[lane] : 0ull;
+        uint64_t s = x;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint64_t y = __shfl_up(s, d);
+            if (lane >= d) s += y;
         }
-        lds[NK * 16] = t ? atomicAdd(ctr, (unsigned long long)t) : 0ull;
+        if (lane < NK * 16) lds[lane] = s - x;
+        if (lane == 63) lds[NK * 16] = s ? atomicAdd(ctr, (unsigned long long)s) : 0ull;
     }
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < NK; ++k) start[k] = lds[NK * 16] + lds[k * 16 + wv] + incl[k] - v[k];
+    __syncthreads();  // lds is reused by the next call
+}
+
+// wg_claim of NC counters at once (counter c = cnt[idx[c]]): one pair of barriers and NC
+// independent atomics in flight together.  A one-workgroup plan (a host-pipeline chunk) is a
+// chain of these claims: nine single claims cost ~30 µs of barriers and atomic round trips.
+// lds: NC·(NK·16 + 1) words.
+template <int NC, int NK>
+__device__ __forceinline__ void wg_claim_n(const uint64_t (&v)[NC][NK], uint64_t (&start)[NC][NK],
+                                           unsigned long long *cnt, const int (&idx)[NC], uint64_t *lds) {
+    constexpr int E = NK * 16;
+    static_assert(E <= 64, "one wave scans the wave totals");
+    const int lane = (int)__lane_id(), wv = threadIdx.x >> 6;
+    uint64_t incl[NC][NK];
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+        for (int k = 0; k < NK; ++k) {
+            uint64_t x = v[c][k];
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint64_t y = __shfl_up(x, d);
+                if (lane >= d) x += y;
+            }
+            incl[c][k] = x;
+            if (lane == 63) lds[c * E + k * 16 + wv] = x;
+        }
+    __syncthreads();
+    if (wv == 0) {
+        uint64_t tot[NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            const uint64_t x = lane < E ? lds[c * E + lane] : 0ull;
+            uint64_t s = x;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint64_t y = __shfl_up(s, d);
+                if (lane >= d) s += y;
+            }
+            if (lane < E) lds[c * E + lane] = s - x;
+            tot[c] = s;
+        }
+        if (lane == 63) {
+            uint64_t r[NC];
+#pragma unroll
+            for (int c = 0; c < NC; ++c) r[c] = tot[c] ? atomicAdd(cnt + idx[c], (unsigned long long)tot[c]) : 0ull;
+#pragma unroll
+            for (int c = 0; c < NC; ++c) lds[NC * E + c] = r[c];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+        for (int k = 0; k < NK; ++k) start[c][k] = lds[NC * E + c] + lds[c * E + k * 16 + wv] + incl[c][k] - v[c][k];
     __syncthreads();  // lds is reused by the next call
 }
 

@@ -1997,9 +1997,13 @@ constexpr uint32_t kPlanThreads = 1024, kPlanPer = 2;  // messages per plan work
 
 #ifndef PSY_ENC_INST_TU  // (defined once, in tdt_api.hip)
 __global__ __launch_bounds__(kPlanThreads) void tdt_encode_plan_kernel(PlanArgs p) {
-    __shared__ uint64_t lds[kPlanPer * 16 + 1];
+    __shared__ uint64_t lds[8 * (kPlanPer * 16 + 1)];
     const uint32_t scap = p.tile_cap / kSpanTiles;
-    uint64_t n[kPlanPer], isl[kPlanPer], T[kPlanPer], S[kPlanPer], j[kPlanPer], t0[kPlanPer], s0[kPlanPer];
+    // the claims' values (A: large messages, tiles, spans; B: the lists) and their starts
+    uint64_t A[3][kPlanPer], SA[3][kPlanPer], B[8][kPlanPer], SB[8][kPlanPer];
+    uint64_t n[kPlanPer];
+    auto &isl = A[0], &T = A[1], &S = A[2];
+    auto &j = SA[0], &t0 = SA[1], &s0 = SA[2];
 #pragma unroll
     for (int k = 0; k < (int)kPlanPer; ++k) {
         const uint32_t i = (blockIdx.x * kPlanPer + k) * kPlanThreads + threadIdx.x;
@@ -2008,12 +2012,12 @@ __global__ __launch_bounds__(kPlanThreads) void tdt_encode_plan_kernel(PlanArgs 
         T[k] = isl[k] ? (n[k] + 16ull * kTileGroups - 1) / (16ull * kTileGroups) : 0;
         S[k] = (T[k] + kSpanTiles - 1) / kSpanTiles;
     }
-    wg_claim<kPlanPer>(isl, j, p.cnt + 2, lds);
-    wg_claim<kPlanPer>(T, t0, p.cnt + 3, lds);
-    wg_claim<kPlanPer>(S, s0, p.cnt + 4, lds);
-    uint64_t sm[kPlanPer], md[kPlanPer], ps[kPlanPer], pm[kPlanPer], sc[kPlanPer], pc[kPlanPer];
-    uint64_t qm[kPlanPer], pq[kPlanPer], qc[kPlanPer], pqc[kPlanPer], bm[kPlanPer], pb[kPlanPer], cp[kPlanPer],
-        pcp[kPlanPer], cc[kPlanPer], pcc[kPlanPer];
+    {
+        constexpr int ia[3] = {2, 3, 4};
+        wg_claim_n<3, kPlanPer>(A, SA, p.cnt, ia, lds);
+    }
+    auto &sm = B[0], &md = B[1], &sc = B[2], &qm = B[3], &qc = B[4], &bm = B[5], &cc = B[6], &cp = B[7];
+    auto &ps = SB[0], &pm = SB[1], &pq = SB[3], &pb = SB[5], &pcp = SB[7];
 #pragma unroll
     for (int k = 0; k < (int)kPlanPer; ++k) {
         const uint32_t i = (blockIdx.x * kPlanPer + k) * kPlanThreads + threadIdx.x;
@@ -2057,14 +2061,10 @@ __global__ __launch_bounds__(kPlanThreads) void tdt_encode_plan_kernel(PlanArgs 
         bm[k] = medium && p.blist && !res_ok ? 1u : 0u;
         md[k] = medium && !bm[k] ? 1u : 0u;
     }
-    wg_claim<kPlanPer>(sm, ps, p.cnt + 0, lds);
-    wg_claim<kPlanPer>(md, pm, p.cnt + 1, lds);
-    wg_claim<kPlanPer>(sc, pc, p.cnt + 5, lds);
-    wg_claim<kPlanPer>(qm, pq, p.cnt + 6, lds);
-    wg_claim<kPlanPer>(qc, pqc, p.cnt + 7, lds);
-    wg_claim<kPlanPer>(bm, pb, p.cnt + 8, lds);
-    wg_claim<kPlanPer>(cc, pcc, p.cnt + 9, lds);
-    wg_claim<kPlanPer>(cp, pcp, p.cnt + 10, lds);
+    {
+        constexpr int ib[8] = {0, 1, 5, 6, 7, 8, 9, 10};
+        wg_claim_n<8, kPlanPer>(B, SB, p.cnt, ib, lds);
+    }
 #pragma unroll
     for (int k = 0; k < (int)kPlanPer; ++k) {
         const uint32_t i = (blockIdx.x * kPlanPer + k) * kPlanThreads + threadIdx.x;

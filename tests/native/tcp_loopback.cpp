@@ -271,6 +271,12 @@ int main(int argc, char **argv) {
         pass(std::min(count, warm * batch), nullptr);
         wire = 0;
     }
+    using PS = TdtSubstrate<PosixTcpSubstrate>::PipeStats;
+    PS tx0{}, rx0{};
+    if (codec == "gpu") {
+        tx0 = tx->pipe_stats();
+        rx0 = rx->pipe_stats();
+    }
     const auto t0 = std::chrono::steady_clock::now();
     pass(count, frames);
     const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
@@ -285,5 +291,18 @@ int main(int argc, char **argv) {
                 codec.c_str(), count, bytes, codec == "gpu" ? batch : (size_t)1, secs, orig / 1e6,
                 double(wire) / 1e6, orig / double(wire), orig / 1e6 / secs, double(wire) / 1e6 / secs, mismatches,
                 warm ? std::min(count, warm * batch) : (size_t)0, half.c_str(), codec == "gpu" ? rxmode.c_str() : "-");
+    if (codec == "gpu") {
+        // where the pipeline threads spent the timed pass (seconds)
+        const PS t = tx->pipe_stats(), r = rx->pipe_stats();
+        std::fprintf(stderr,
+                     "{\"pipe\": {\"encode\": %.4f, \"encode_calls\": %llu, \"tx_wait\": %.4f, \"send\": %.4f, "
+                     "\"recv\": %.4f, \"rx_sleep\": %.4f, \"rx_wait\": %.4f, \"decode\": %.4f, \"decode_calls\": %llu, "
+                     "\"decode_MB\": %.1f, \"dec_wait\": %.4f, \"deliver_wait\": %.4f}}\n",
+                     t.encode - tx0.encode, (unsigned long long)(t.encode_calls - tx0.encode_calls), t.tx_wait - tx0.tx_wait,
+                     t.send - tx0.send, r.recv - rx0.recv, r.rx_sleep - rx0.rx_sleep, r.rx_wait - rx0.rx_wait,
+                     r.decode - rx0.decode, (unsigned long long)(r.decode_calls - rx0.decode_calls),
+                     double(r.decode_bytes - rx0.decode_bytes) / 1e6, r.dec_wait - rx0.dec_wait,
+                     r.deliver_wait - rx0.deliver_wait);
+    }
     return mismatches ? 1 : 0;
 }

@@ -275,9 +275,10 @@ def test_large_message(n, lead):
 
 @pytest.mark.timeout(300)
 def test_host_pipeline_multichunk():
-    """tdt_encode_host / tdt_decode_host (pinned staging, two pipeline streams) on a batch of
-    ~600 MB, so it is cut into three 256 MiB chunks that alternate between the two slots: every
-    blob equals the oracle's, the decode restores the input, and no chunk raised a device flag."""
+    """tdt_encode_host / tdt_decode_host (pageable caller buffers: pinned staging) on a batch of
+    ~600 MB of messages <= 64 KiB, so the one-pass encode runs over ten 64 MiB chunks rotating
+    through the four pipeline slots: every blob equals the oracle's, the decode restores the input,
+    and no chunk raised a device flag."""
     rng = np.random.default_rng(77)
     sizes = np.concatenate([rng.integers(1, 65, 2000) * 64, np.full(9000, 65536, np.int64)])
     rng.shuffle(sizes)
@@ -296,4 +297,53 @@ def test_host_pipeline_multichunk():
     dec, doff, dst = codec.decode_host(enc, eoff, int(off[-1]))
     assert int(np.abs(dst).sum()) == 0
     assert np.array_equal(doff, off) and np.array_equal(dec, buf)
+    assert codec.error_flags() == 0
+
+
+@pytest.mark.timeout(300)
+def test_host_pipeline_slotted_pinned():
+    """A socket-sized batch of 1 MiB messages (the C1 substrate's send_batch) through the host
+    pipeline: messages over 64 KiB take the slotted class kernels (tiles) and the gather straight
+    into the host buffer.  Pinned caller buffers (direct DMA, output written by the gather kernel
+    through the mapped pointer) and pageable ones (staging) give the same blobs, equal to the
+    oracle's; both decode back; a too-small output buffer is TDT_E_CAPACITY."""
+    import ctypes as C
+    from psyne_amd._lib import TDT_E_CAPACITY, check
+    rng = np.random.default_rng(123)
+    sizes = np.array([1 << 20] * 40 + list(rng.integers(1, 256, 60) * 64) + [3 << 20, 4, 65536 + 64], np.int64)
+    rng.shuffle(sizes)
+    off = np.zeros(sizes.size + 1, np.uint64)
+    off[1:] = np.cumsum(sizes)
+    x = rng.normal(0, 0.01, int(off[-1]) // 4).astype(np.float32)
+    x[rng.random(x.size) < 0.7] = 0
+    buf = x.view(np.uint8)
+    codec = make_codec()
+    enc, eoff, st = codec.encode_host(buf, off)  # pageable
+    assert int(np.abs(st).sum()) == 0
+    orc = Oracle()
+    for i in list(range(6)) + list(range(sizes.size - 6, sizes.size)) + [int(np.argmax(sizes))]:
+        assert enc[eoff[i]:eoff[i + 1]].tobytes() == orc.encode(buf[off[i]:off[i + 1]], bandwidth=10.0), "blob %d" % i
+    n = sizes.size
+    cap = int(sum(codec.encode_bound(int(s)) for s in sizes))
+    pin_in = torch.from_numpy(buf).pin_memory()
+    pin_out = torch.empty(cap, dtype=torch.uint8).pin_memory()
+    poff = np.zeros(n + 1, np.uint64)
+    pst = np.zeros(n, np.int32)
+    check(codec._lib.tdt_encode_host(codec._h, pin_in.data_ptr(), off.ctypes.data, n, pin_out.data_ptr(), cap,
+                                     poff.ctypes.data, pst.ctypes.data))
+    assert int(np.abs(pst).sum()) == 0 and np.array_equal(poff, eoff)
+    assert np.array_equal(pin_out[: int(poff[-1])].numpy(), enc[: int(eoff[-1])])
+    dec, doff, dst = codec.decode_host(enc, eoff, int(off[-1]))
+    assert int(np.abs(dst).sum()) == 0 and np.array_equal(doff, off) and np.array_equal(dec, buf)
+    pin_dec = torch.empty(int(off[-1]), dtype=torch.uint8).pin_memory()
+    doff2 = np.zeros(n + 1, np.uint64)
+    dst2 = np.zeros(n, np.int32)
+    check(codec._lib.tdt_decode_host(codec._h, pin_out.data_ptr(), poff.ctypes.data, n, pin_dec.data_ptr(),
+                                     int(off[-1]), doff2.ctypes.data, dst2.ctypes.data))
+    assert int(np.abs(dst2).sum()) == 0 and np.array_equal(doff2, off)
+    assert torch.equal(pin_dec, pin_in)
+    small = np.empty(int(eoff[-1]) // 2, np.uint8)
+    r = codec._lib.tdt_encode_host(codec._h, buf.ctypes.data, off.ctypes.data, n, small.ctypes.data, small.size,
+                                   poff.ctypes.data, pst.ctypes.data)
+    assert r == TDT_E_CAPACITY
     assert codec.error_flags() == 0
