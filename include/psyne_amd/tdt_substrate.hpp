@@ -277,15 +277,19 @@ public:
     ~PinnedBuffer() { tdt_host_free(p_); }
     PinnedBuffer(const PinnedBuffer &) = delete;
     PinnedBuffer &operator=(const PinnedBuffer &) = delete;
+    // (contents are not kept; a growth takes 1.5x and whole 2 MiB: pinning tens of MB costs
+    // milliseconds, so a buffer should grow rarely)
     void reserve(size_t bytes) {
         if (bytes <= cap_) return;
+        const size_t want = std::max(bytes, cap_ + cap_ / 2);
+        const size_t cap = (want + (2u << 20) - 1) & ~size_t((2u << 20) - 1);
         tdt_host_free(p_);
         p_ = nullptr;
         cap_ = 0;
         void *q = nullptr;
-        if (tdt_host_alloc(bytes, &q) != TDT_OK) throw std::bad_alloc();
+        if (tdt_host_alloc(cap, &q) != TDT_OK) throw std::bad_alloc();
         p_ = static_cast<uint8_t *>(q);
-        cap_ = bytes;
+        cap_ = cap;
     }
     uint8_t *data() { return p_; }
     size_t capacity() const { return cap_; }
@@ -470,7 +474,17 @@ public:
         static_assert(sizeof(size_t) == sizeof(uint64_t), "size_t is 64-bit");
         if (n == 0) return 0;
         rethrow_tx();
-        if (!tx_thread_.joinable()) tx_thread_ = std::thread([this] { tx_loop(); });
+        if (!tx_thread_.joinable()) {
+            // every ring buffer pinned up front for the first sub-batch's size (not one by one
+            // inside later, timed sends)
+            uint64_t cap = 0, payload = 0;
+            for (size_t i = 0; i < n && (i == 0 || payload + sizes[i] <= kSubBytes) && i < kSubFrames; ++i) {
+                payload += sizes[i];
+                cap += tdt_encode_bound(sizes[i], codec_.word_size());
+            }
+            for (auto &t : tx_ring_) t.mem.reserve(cap);
+            tx_thread_ = std::thread([this] { tx_loop(); });
+        }
         const auto *msgs = reinterpret_cast<const uint8_t *const *>(data);
         const auto *sz = reinterpret_cast<const uint64_t *>(sizes);
         if (record_last_) {
@@ -840,6 +854,14 @@ private:
             rx_max_msg_ = std::max<uint64_t>(rx_max_msg_, max_msg);
         }
         if (!rx_thread_.joinable()) {
+            // the read-ahead ring pinned up front (frames and payloads of a full buffer at a
+            // 1.5x decoded/wire ratio; larger payloads grow a buffer once)
+            const uint64_t fcap = frame_capacity(max_msg);
+            while (rx_pool_.size() < kRing + 1) {
+                rx_pool_.push_back(std::make_unique<RxBuf>());
+                rx_pool_.back()->mem.reserve(std::max<uint64_t>(kRxBytes + fcap, 2 * fcap));
+                rx_pool_.back()->dec.reserve(kRxBytes + kRxBytes / 2);
+            }
             dec_thread_ = std::thread([this] { dec_loop(); });
             rx_thread_ = std::thread([this] { rx_loop(); });
         }

@@ -114,6 +114,10 @@ struct PlanWS {
     // the large-message pipeline runs on `side` beside the medium/small lists (fork/join events)
     hipStream_t side = nullptr;
     hipEvent_t fork = nullptr, join = nullptr;
+    // host-pipeline slots run without the side stream: their chunks already overlap one another,
+    // and every extra stream shares HIP's few hardware queues with the other slots (and with the
+    // other end's context in a one-process loopback: C1's encode 6.2 -> 4.0 ms per 50 MiB call)
+    bool no_side = false;
     void release() {
         if (join) (void)hipEventDestroy(join);
         if (fork) (void)hipEventDestroy(fork);
@@ -493,7 +497,7 @@ int launch_slotted(tdt_ctx *c, PlanWS &pw, psy::EncodeArgs a, hipStream_t s) {
     // list (queued behind it on one stream they would run alone in its tail)
     const bool medium_on = !H.valid || H.v[2] + H.v[16] > 0;  // (counters 1 and 8)
     if (tiles_on || ((small_on || mid_on || copy_on) && medium_on && !c->small_main)) {
-        const int fr = c->no_side ? -1 : fork_side(pw, s);
+        const int fr = c->no_side || pw.no_side ? -1 : fork_side(pw, s);
         if (fr > 0) return fr;
         forked = fr == TDT_OK;
         if (forked) ts = pw.side;
@@ -828,7 +832,7 @@ int launch_decode_slotted(tdt_ctx *c, PlanWS &pw, psy::DecodeArgs a, hipStream_t
     // list (the small list queued behind the main list ran alone in its tail: C4 1.6 ms)
     const bool main_on = !H.valid || H.v[0] + H.v[12] > 0;  // (counters 0 and 6)
     if (large_on || ((small_on || copy_on) && main_on && !c->small_main)) {
-        const int fr = c->no_side ? -1 : fork_side(pw, s);
+        const int fr = c->no_side || pw.no_side ? -1 : fork_side(pw, s);
         if (fr > 0) return fr;
         forked = fr == TDT_OK;
         if (forked) ts = pw.side;
@@ -957,25 +961,33 @@ bool is_pinned(const void *p) {
 int ensure_slot(tdt_ctx *c, int k, size_t dev_bytes, size_t pin_words, size_t sin, size_t sout) {
     auto &h = c->hs[k];
     if (!h.stream) {
+        h.pw.no_side = true;
         HIPCHK(hipStreamCreateWithFlags(&h.stream, hipStreamNonBlocking));
         HIPCHK(hipEventCreateWithFlags(&h.ev, hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&h.evc, hipEventDisableTiming));
         HIPCHK(hipHostMalloc(&h.flag, 4, hipHostMallocDefault));
         *h.flag = 0;
     }
+    // growth takes 1.5x (whole MiB): a hipFree waits for the whole device (every stream, other
+    // contexts' too) and pinning host memory costs milliseconds, so buffers sized by the chunks
+    // of varying calls should settle after a few
+    auto grown = [](size_t need, size_t have) {
+        return (std::max(need, have + have / 2) + (1u << 20) - 1) & ~size_t((1u << 20) - 1);
+    };
     if (dev_bytes > h.dev_bytes) {
+        const size_t cap = grown(dev_bytes, h.dev_bytes);
         if (h.dev) HIPCHK(hipFree(h.dev));
         h.dev = nullptr;
         h.dev_bytes = 0;
-        HIPCHK(hipMalloc(&h.dev, dev_bytes));
-        h.dev_bytes = dev_bytes;
+        HIPCHK(hipMalloc(&h.dev, cap));
+        h.dev_bytes = cap;
     }
-    auto pinned = [](uint8_t *&buf, size_t &have, size_t need) -> int {
+    auto pinned = [&](uint8_t *&buf, size_t &have, size_t need) -> int {
         if (need <= have) return TDT_OK;
+        const size_t cap = grown(need, have);
         if (buf) HIPCHK(hipHostFree(buf));
         buf = nullptr;
         have = 0;
-        const size_t cap = std::max(need, have * 2);
         HIPCHK(hipHostMalloc(&buf, cap, hipHostMallocDefault));
         have = cap;
         return TDT_OK;
@@ -1207,6 +1219,11 @@ int host_encode(tdt_ctx *c, const uint8_t *h_in, const uint64_t *h_in_off, uint3
                 const uint64_t *sizes = nullptr) {
     const int ws = c->cfg.word_size;
     const bool pin_in = !msgs && is_pinned(h_in + h_in_off[0]);
+    // gather input from pinned caller buffers (a channel's pinned message memory): DMA'd run by
+    // run of adjacent messages instead of staged by the copy pool (checked for calls of up to
+    // 4096 messages; a pointer-attribute query per message)
+    bool msgs_pinned = msgs && n_msgs <= 4096;
+    for (uint32_t i = 0; i < n_msgs && msgs_pinned; ++i) msgs_pinned = sizes[i] == 0 || is_pinned(msgs[i]);
     // a pinned caller buffer receives the chunks' output straight from the copy kernels
     uint8_t *d_out = nullptr;
     if (is_pinned(h_out) && hipHostGetDevicePointer(reinterpret_cast<void **>(&d_out), h_out, 0) != hipSuccess) {
@@ -1237,7 +1254,8 @@ int host_encode(tdt_ctx *c, const uint8_t *h_in, const uint64_t *h_in_off, uint3
         const Chunk &k = ch[ci];
         const int si = (int)(ci % kHostSlots);
         auto &h = c->hs[si];
-        int st = ensure_slot(c, si, chunk_dev_bytes(k), chunk_pin_words(k), pin_in ? 0 : k.in_bytes, pin_out ? 0 : k.cap);
+        int st = ensure_slot(c, si, chunk_dev_bytes(k), chunk_pin_words(k), pin_in || msgs_pinned ? 0 : k.in_bytes,
+                             pin_out ? 0 : k.cap);
         if (st) return st;
         st = sync_slot(c, h);  // the slot's previous chunk is done with its buffers
         if (st) return st;
@@ -1252,10 +1270,10 @@ int host_encode(tdt_ctx *c, const uint8_t *h_in, const uint64_t *h_in_off, uint3
             }
         }
         const uint8_t *src = msgs ? nullptr : h_in + b0;
-        if (msgs) {
+        if (msgs && !msgs_pinned) {
             c->pool->gather(h.stage_in, msgs + k.m0, sizes + k.m0, k.n);
             src = h.stage_in;
-        } else if (!pin_in) {
+        } else if (!msgs && !pin_in) {
             c->pool->copy(h.stage_in, src, k.in_bytes);
             src = h.stage_in;
         }
@@ -1265,7 +1283,18 @@ int host_encode(tdt_ctx *c, const uint8_t *h_in, const uint64_t *h_in_off, uint3
         auto *dooff = reinterpret_cast<uint64_t *>(d + k.o_ooff);
         auto *dst = reinterpret_cast<int32_t *>(d + k.o_st);
         auto *dlen = reinterpret_cast<uint64_t *>(d + k.o_len);
-        HIPCHK(hipMemcpyAsync(d, src, k.in_bytes, hipMemcpyHostToDevice, h.stream));
+        if (src) {
+            HIPCHK(hipMemcpyAsync(d, src, k.in_bytes, hipMemcpyHostToDevice, h.stream));
+        } else {
+            for (uint32_t i = 0; i < k.n;) {
+                const uint8_t *p0 = msgs[k.m0 + i];
+                uint64_t len = sizes[k.m0 + i];
+                uint32_t j = i + 1;
+                while (j < k.n && msgs[k.m0 + j] == p0 + len) len += sizes[k.m0 + j++];
+                if (len) HIPCHK(hipMemcpyAsync(d + pin_in_off[i], p0, len, hipMemcpyHostToDevice, h.stream));
+                i = j;
+            }
+        }
         // in_off and (slotted) the slots: one copy
         HIPCHK(hipMemcpyAsync(doff, pin_in_off, (k.scap ? 16ull : 8ull) * (k.n + 1), hipMemcpyHostToDevice, h.stream));
         if (k.scap) {

@@ -25,7 +25,9 @@
 // check every wire blob against the oracle.  Effective throughput = original bytes / wall time
 // from the first send to the last verified receive (the reference's "Effective throughput ...
 // MB/s (original)", :401-403), after an untimed warm-up pass of --warm batches (default 2: the
-// first calls of each end allocate its workspaces and pinned staging).  One JSON line on stdout.
+// first calls of each end allocate its workspaces and pinned staging).  --mem pinned puts the
+// tensors in pinned host memory (as a channel's message buffers could be) for every row.  One
+// JSON line on stdout.
 #include <dlfcn.h>
 
 #include <psyne_amd/tdt_substrate.hpp>
@@ -78,6 +80,9 @@ int main(int argc, char **argv) {
     // gpu receiver: "views" (receive_batch_views: payloads checked in the pipeline's pinned
     // buffers, zero-copy) or "copy" (receive_batch into a std::vector)
     std::string rxmode = "views";
+    // the tensors' memory, for every row: "pageable" (std::vector, default) or "pinned"
+    // (tdt_host_alloc: the GPU row's encode DMAs them directly instead of staging them)
+    std::string mem = "pageable";
     int port = 18080;
     std::string codec = "gpu", dump;
     for (int i = 1; i + 1 < argc; i += 2) {
@@ -91,10 +96,19 @@ int main(int argc, char **argv) {
         else if (k == "--warm") warm = std::stoul(v);
         else if (k == "--half") half = v;
         else if (k == "--rx") rxmode = v;
+        else if (k == "--mem") mem = v;
     }
     const size_t bytes = floats * 4;
     // payloads (GRADIENTS: 70 % zeros, N(0, 0.01) otherwise)
-    std::vector<std::vector<uint8_t>> msgs(count, std::vector<uint8_t>(bytes));
+    std::vector<std::vector<uint8_t>> pageable(mem == "pinned" ? 0 : count, std::vector<uint8_t>(bytes));
+    PinnedBuffer pinned;
+    if (mem == "pinned") pinned.reserve(count * bytes);
+    struct Msg {
+        uint8_t *p;
+        uint8_t *data() const { return p; }
+    };
+    std::vector<Msg> msgs(count);
+    for (size_t i = 0; i < count; ++i) msgs[i].p = mem == "pinned" ? pinned.data() + i * bytes : pageable[i].data();
     {
         std::mt19937_64 rng(0x5EED0001);
         std::normal_distribution<float> nd(0.0f, 0.01f);
@@ -140,7 +154,7 @@ int main(int argc, char **argv) {
     FILE *frames = nullptr;
     if (!dump.empty()) {
         FILE *f = std::fopen((dump + "/inputs.bin").c_str(), "wb");
-        for (auto &m : msgs) std::fwrite(m.data(), 1, m.size(), f);
+        for (auto &m : msgs) std::fwrite(m.data(), 1, bytes, f);
         std::fclose(f);
         frames = std::fopen((dump + "/frames.bin").c_str(), "wb");
     }
@@ -287,10 +301,11 @@ int main(int argc, char **argv) {
     std::printf("{\"harness\": \"tcp_loopback\", \"codec\": \"%s\", \"tensors\": %zu, \"tensor_bytes\": %zu, "
                 "\"batch\": %zu, \"seconds\": %.4f, \"original_MB\": %.1f, \"wire_MB\": %.1f, "
                 "\"compression_ratio\": %.4f, \"effective_MBps\": %.1f, \"network_MBps\": %.1f, "
-                "\"mismatches\": %zu, \"warmup_tensors\": %zu, \"half\": \"%s\", \"rx\": \"%s\"}\n",
+                "\"mismatches\": %zu, \"warmup_tensors\": %zu, \"half\": \"%s\", \"rx\": \"%s\", \"mem\": \"%s\"}\n",
                 codec.c_str(), count, bytes, codec == "gpu" ? batch : (size_t)1, secs, orig / 1e6,
                 double(wire) / 1e6, orig / double(wire), orig / 1e6 / secs, double(wire) / 1e6 / secs, mismatches,
-                warm ? std::min(count, warm * batch) : (size_t)0, half.c_str(), codec == "gpu" ? rxmode.c_str() : "-");
+                warm ? std::min(count, warm * batch) : (size_t)0, half.c_str(), codec == "gpu" ? rxmode.c_str() : "-",
+                mem.c_str());
     if (codec == "gpu") {
         // where the pipeline threads spent the timed pass (seconds)
         const PS t = tx->pipe_stats(), r = rx->pipe_stats();

@@ -616,3 +616,48 @@ def test_encode_host_gather(orc):
     assert int(np.abs(st).sum()) == 0
     for i, m in enumerate(msgs):
         assert out[ooff[i]:ooff[i + 1]].tobytes() == orc.encode(m, bandwidth=10.0), "message %d (%d B)" % (i, m.size)
+
+
+def test_encode_host_gather_pinned(orc):
+    """tdt_encode_host_v over messages in pinned memory (a channel's pinned message buffers): no
+    staging, one DMA per run of adjacent messages (runs broken by gaps and by a reversed order),
+    blobs equal to the oracle's; then the same messages pageable give the same bytes."""
+    import ctypes as C
+    from psyne_amd._lib import check
+    rng = np.random.default_rng(98)
+    sizes = [1 << 20] * 12 + list(rng.integers(1, 2048, 40) * 4) + [65536] * 6 + [0, 12]
+    total = sum(sizes) + 4096 * len(sizes)
+    pin = torch.empty(total, dtype=torch.uint8).pin_memory()
+    host = pin.numpy()
+    starts, pos = [], 0
+    for k, n in enumerate(sizes):
+        starts.append(pos)
+        pos += n + (4096 if k % 5 == 4 else 0)  # every fifth message leaves a gap (a new run)
+    order = list(range(len(sizes)))
+    order[20:30] = order[20:30][::-1]  # not in memory order: each of these starts a run
+    msgs = []
+    for k in order:
+        n = sizes[k]
+        host[starts[k]:starts[k] + n] = grad(rng, n // 4).view(np.uint8)[:n] if n % 4 == 0 else rng.integers(0, 256, n)
+        msgs.append((int(starts[k]), int(n)))
+    n = len(msgs)
+    codec = make_codec()
+    base = pin.data_ptr()
+    ptrs = (C.c_void_p * n)(*[int(base + a) for a, _ in msgs])
+    sz = np.array([b for _, b in msgs], np.uint64)
+    cap = int(sum(codec.encode_bound(int(b)) for b in sz))
+    out = np.empty(cap, np.uint8)
+    ooff = np.zeros(n + 1, np.uint64)
+    st = np.zeros(n, np.int32)
+    check(codec._lib.tdt_encode_host_v(codec._h, C.addressof(ptrs), sz.ctypes.data, n, out.ctypes.data, cap,
+                                       ooff.ctypes.data, st.ctypes.data))
+    assert int(np.abs(st).sum()) == 0
+    for i, (a, b) in enumerate(msgs):
+        assert out[ooff[i]:ooff[i + 1]].tobytes() == orc.encode(host[a:a + b].copy(), bandwidth=10.0), "message %d" % i
+    copies = [np.array(host[a:a + b]) for a, b in msgs]
+    ptrs2 = (C.c_void_p * n)(*[m.ctypes.data for m in copies])
+    out2 = np.empty(cap, np.uint8)
+    ooff2 = np.zeros(n + 1, np.uint64)
+    check(codec._lib.tdt_encode_host_v(codec._h, C.addressof(ptrs2), sz.ctypes.data, n, out2.ctypes.data, cap,
+                                       ooff2.ctypes.data, st.ctypes.data))
+    assert np.array_equal(ooff2, ooff) and np.array_equal(out2[: int(ooff[-1])], out[: int(ooff[-1])])
