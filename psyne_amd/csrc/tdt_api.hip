@@ -348,7 +348,9 @@ uint32_t tile_cap_of(int ws) { return (262144u / (uint32_t)ws) * psy::kSpanTiles
 constexpr uint32_t kL0 = 1024, kT0 = 8192;
 size_t elarge_bytes(uint32_t lcap, uint32_t tcap, int ws) {
     const size_t sc = tcap / psy::kSpanTiles;
-    return (size_t)lcap * sizeof(psy::LMeta) + (size_t)tcap * (8 + sizeof(psy::TileRec)) + sc * 8 + sc * ws * 1024;
+    // LMeta | tile entries | tile records | span entries | span bins | count-pass tile list
+    return (size_t)lcap * sizeof(psy::LMeta) + (size_t)tcap * (8 + sizeof(psy::TileRec)) + sc * 8 + sc * ws * 1024 +
+           (size_t)tcap * 8;
 }
 uint32_t pow2_at_least(uint64_t x, uint32_t lo, uint32_t hi) {
     uint64_t p = lo;
@@ -474,6 +476,7 @@ int launch_slotted(tdt_ctx *c, PlanWS &pw, psy::EncodeArgs a, hipStream_t s) {
     auto *spans =
         reinterpret_cast<uint64_t *>(reinterpret_cast<uint8_t *>(trec) + sizeof(psy::TileRec) * pw.e_tcap);
     auto *shist = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(spans) + 8ull * (pw.e_tcap / psy::kSpanTiles));
+    auto *rtiles = reinterpret_cast<uint64_t *>(shist + (size_t)(pw.e_tcap / psy::kSpanTiles) * WS * 256);
     HIPCHK(hipMemsetAsync(cnt, 0, 128, s));
     psy::PlanArgs p{a.in,      a.in_off,  n,       cnt64,   slist,          mlist,              qlist,
                     blist,     clist,   tiles,   spans,          lmeta,              lcap,
@@ -483,7 +486,8 @@ int launch_slotted(tdt_ctx *c, PlanWS &pw, psy::EncodeArgs a, hipStream_t s) {
     hipLaunchKernelGGL(psy::tdt_encode_plan_kernel, dim3((uint32_t)(((uint64_t)n + per - 1) / per)),
                        dim3(psy::kPlanThreads), 0, s, p);
     HIPCHK(hipGetLastError());
-    if (!capturing && (st = record_counts(H, cnt, n, s))) return st;
+    // (with tiles, the snapshot follows the map pass instead: it also holds the count pass's list length)
+    if (!capturing && !tiles_on && (st = record_counts(H, cnt, n, s))) return st;
     a.pcnt = cnt;
     const uint32_t ovf512 = (uint32_t)c->cus * 3, ovf256 = (uint32_t)c->cus * 6, ovf64 = (uint32_t)c->cus * 24;
     // main launch over [0, g) + overflow launch over [g, count) of one class
@@ -508,6 +512,8 @@ int launch_slotted(tdt_ctx *c, PlanWS &pw, psy::EncodeArgs a, hipStream_t s) {
         a.lmeta = lmeta;
         a.trec = trec;
         a.shist = shist;
+        a.rtiles = rtiles;
+        a.rcount = cnt64 + 11;
         a.lcap = lcap;
         a.tcap = tcap;
 #define PSY_TILE_STEP(TL, IDX, BOUND)                                                                           \
@@ -522,9 +528,10 @@ int launch_slotted(tdt_ctx *c, PlanWS &pw, psy::EncodeArgs a, hipStream_t s) {
                  hipLaunchKernelGGL((psy::tdt_encode_kernel<WS, 512, 8, MODE_ENCODE, 0, TL, 1>), dim3(g), dim3(512), \
                                     0, ts, a);                                                                  \
              })
-        PSY_TILE_STEP(1, 8, scap);  // span histograms
-        PSY_TILE_STEP(4, 4, lcap);  // mapping per large message
-        PSY_TILE_STEP(2, 6, tcap);  // per-tile counts
+        PSY_TILE_STEP(1, 8, scap);  // span histograms (and counts under the speculated mapping)
+        PSY_TILE_STEP(4, 4, lcap);  // mapping per large message; lists the tiles to count again
+        if (!capturing && (st = record_counts(H, cnt, n, ts))) return st;
+        PSY_TILE_STEP(2, 22, tcap);  // per-tile counts of the listed tiles
         hipLaunchKernelGGL((psy::tdt_encode_lscan_kernel<WS>), dim3(std::max(1u, std::min(lcap, 1024u))), dim3(64), 0,
                            ts, a, cnt + 4, lcap);
         PSY_TILE_STEP(3, 6, tcap);  // emit

@@ -119,6 +119,11 @@ struct EncodeArgs {
     LMeta *lmeta;
     TileRec *trec;
     uint32_t *shist;  // per span: WS x 256 bin counts
+    // the count pass's work list, appended by the map pass: every tile of a message whose mapping
+    // is not the speculated one, and the tiles whose fused count could not rule the 255-cap out
+    // (entries as `tiles`; its length is plan counter 11, u32 view pcnt[22])
+    uint64_t *rtiles;
+    unsigned long long *rcount;
 };
 
 template <int WS, int TEAM>
@@ -970,10 +975,27 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
             return;
         }
         if constexpr (TL == 4) {
-            if (tid == 0) {
-                uint32_t bits = 0;
-                for (int b = 0; b < WS; ++b) bits |= wm[M_MAP + b] << b;
-                a.lmeta[lj].mapbits = bits;
+            uint32_t bits = 0;
+            for (int b = 0; b < WS; ++b) bits |= wm[M_MAP + b] << b;
+            if (tid == 0) a.lmeta[lj].mapbits = bits;
+            {
+                // the count pass's list (one workgroup per listed tile, instead of one per tile
+                // that mostly exits at once: C4's count launch was 2 ms of such workgroups);
+                // word sizes without a speculated mapping list every tile
+                const uint32_t nt = a.lmeta[lj].ntiles, t0 = a.lmeta[lj].tile0;
+                const bool miss = kSpec == 0xffffffffu || bits != kSpec;
+                for (uint32_t t = (uint32_t)tid; t < nt; t += TEAM) {
+                    const bool need = miss || a.trec[t0 + t].clean == kRecount;
+                    const uint64_t bal = __ballot(need);
+                    if (bal == 0) continue;
+                    const int first = __ffsll((unsigned long long)bal) - 1;
+                    uint32_t base = 0;
+                    if (lane == first) base = (uint32_t)atomicAdd(a.rcount, (unsigned long long)__popcll(bal));
+                    base = (uint32_t)__shfl((int)base, first);
+                    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+                    if (need) a.rtiles[base + rank] = ((uint64_t)t << 32) | lj;
+                }
             }
             return;
         }
@@ -1917,6 +1939,7 @@ __device__ __forceinline__ uint32_t entry_count(const EncodeArgs &a) {
     if constexpr (TL == 0) c = *a.list_count + (a.list2 ? *a.list2_count : 0u);
     else if constexpr (TL == 4) c = umin(a.pcnt[4], a.lcap);
     else if constexpr (TL == 1) c = umin(a.pcnt[8], a.tcap / kSpanTiles);
+    else if constexpr (TL == 2) c = umin(a.pcnt[22], a.tcap);
     else c = umin(a.pcnt[6], a.tcap);
     return __builtin_amdgcn_readfirstlane(c);
 }
@@ -1942,7 +1965,7 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(E
                 const uint32_t msg = a.lmeta[i].msg;  // one large message per workgroup
                 if (msg != kNone) encode_one<WS, TEAM, G, MODE, LB, TL>(a, smem, msg, i, 0);
             } else {
-                const uint64_t e = TL == 1 ? a.spans[i] : a.tiles[i];  // one span (TL 1) or tile
+                const uint64_t e = TL == 1 ? a.spans[i] : TL == 2 ? a.rtiles[i] : a.tiles[i];  // a span or tile
                 const uint32_t lj = (uint32_t)e;
                 if (lj == kNone) return;  // a message that did not fit the budgets
                 encode_one<WS, TEAM, G, MODE, LB, TL>(a, smem, a.lmeta[lj].msg, lj, (uint32_t)(e >> 32));

@@ -254,3 +254,18 @@ def test_compacted_offsets_past_4gib():
     torch.cuda.synchronize()
     assert int(dst.abs().sum()) == 0 and torch.equal(back, data)
     assert torch.equal(doff, off)
+
+
+@pytest.mark.timeout(300)
+def test_count_list_history_on_warm_context():
+    """The count pass runs over the tiles the map pass lists (a message whose mapping is not the
+    speculated one, or a tile whose fused count could not rule the 255-cap out); its grid comes
+    from the previous call's list length.  One warm context alternates batches whose list is
+    empty (gradients: the speculation holds), long (runs data: every tile) and mixed — every
+    blob equals the oracle's each time."""
+    rng = np.random.default_rng(31)
+    codec = codec_for(4)
+    grads = [gradient(rng, 1 << 20) for _ in range(6)]
+    runs = [runs_message(rng, (1 << 20) + 4 * 77, 300) for _ in range(5)]
+    for batch in (grads, runs, grads, grads + runs[:2] + [np.zeros(3 << 20, np.uint8)], runs):
+        check_batch(batch, codec=codec)
