@@ -2022,6 +2022,16 @@ constexpr uint32_t kPlanThreads = 1024, kPlanPer = 2;  // messages per plan work
 __global__ __launch_bounds__(kPlanThreads) void tdt_encode_plan_kernel(PlanArgs p) {
     __shared__ uint64_t lds[8 * (kPlanPer * 16 + 1)];
     const uint32_t scap = p.tile_cap / kSpanTiles;
+    // A message takes the tiled path above max(large_min, 1/4096 of the batch's bytes), as the
+    // decode plan: below that the batch has enough other messages to keep the chip busy while
+    // one 512-lane team streams it (long messages are dispatched first), and the streaming body
+    // reads it twice like the tiles but without their span / map / scan passes — C4 (1 MiB
+    // messages in 24.6 GiB) encode 19.7 -> 18.8 ms with none of its messages tiled.
+    uint64_t thr = p.large_min;
+    if (p.n_msgs) {
+        const uint64_t share = (p.in_off[p.n_msgs] - p.in_off[0]) / 4096;
+        thr = share > thr ? share : thr;
+    }
     // the claims' values (A: large messages, tiles, spans; B: the lists) and their starts
     uint64_t A[3][kPlanPer], SA[3][kPlanPer], B[8][kPlanPer], SB[8][kPlanPer];
     uint64_t n[kPlanPer];
@@ -2031,7 +2041,7 @@ __global__ __launch_bounds__(kPlanThreads) void tdt_encode_plan_kernel(PlanArgs 
     for (int k = 0; k < (int)kPlanPer; ++k) {
         const uint32_t i = (blockIdx.x * kPlanPer + k) * kPlanThreads + threadIdx.x;
         n[k] = i < p.n_msgs ? p.in_off[i + 1] - p.in_off[i] : 0;
-        isl[k] = i < p.n_msgs && n[k] > p.large_min ? 1u : 0u;
+        isl[k] = i < p.n_msgs && n[k] > thr ? 1u : 0u;
         T[k] = isl[k] ? (n[k] + 16ull * kTileGroups - 1) / (16ull * kTileGroups) : 0;
         S[k] = (T[k] + kSpanTiles - 1) / kSpanTiles;
     }

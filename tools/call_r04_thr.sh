@@ -1,0 +1,7 @@
+#!/bin/bash
+set -u
+OUT=gpurun_out/r04_thr; mkdir -p $OUT
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_large.py tests/test_gpu_scale.py -k "large or c4 or tile or runs or zipf or host" > $OUT/tests.log 2>&1 || { echo TESTFAIL; grep -E "FAILED|Error|assert" $OUT/tests.log | head -20; tail -5 $OUT/tests.log; exit 1; }
+tail -2 $OUT/tests.log
+for r in 1 2 3; do bash tools/exp_run_wl.sh r04_thr c4 base thr || exit 1; done
+bash tools/exp_run_wl.sh r04_thr c3 base thr
