@@ -435,6 +435,9 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
     // the histogram pass counts run starts under the speculated mapping: tiled messages (TL 1,
     // one wave per tile) and streaming whole messages (TL 0)
     constexpr bool SPECA1 = kSpec != 0xffffffffu && MODE == MODE_ENCODE && (TL == 0 || TL == 1);
+    // streaming rounds in flight per wave: the streaming-only kernel and the span pass have the
+    // registers (37 / 30 VGPRs with one); kernels holding the resident body too keep one
+    constexpr int PF = PATH == PATH_STREAM || TL == 1 ? 4 : 1;
     if constexpr (TL == 2 && kSpec != 0xffffffffu) {
         // the span pass counted this tile under the speculated mapping and it is the real one
         const LMeta &lm = a.lmeta[lj];
@@ -512,11 +515,38 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
             for (int r = 0; r < G; ++r)
                 if ((uint32_t)r < RW) body((uint32_t)r, dres[r], cres[r], std::true_type{});
         } else {
-            for (uint32_t r = 0; r < RW; ++r) {
-                if (16ull * (gw0 + r * 64) >= n) break;  // (uniform) no group of the message left
-                uint4 d = load_group(gw0 + r * 64 + lane);
-                uint32_t c = 0;
-                body(r, d, c, std::false_type{});
+            // rounds r < RW of the wave that hold a group of the message (uniform)
+            auto live = [&](uint32_t r) __attribute__((always_inline)) {
+                return r < RW && 16ull * (gw0 + r * 64) < n;
+            };
+            if constexpr (PF == 1) {
+                for (uint32_t r = 0; live(r); ++r) {
+                    uint4 d = load_group(gw0 + r * 64 + lane);
+                    uint32_t c = 0;
+                    body(r, d, c, std::false_type{});
+                }
+            } else {
+                // PF rounds in flight: round r + PF is loaded before round r is processed (one
+                // load per round and its full HBM latency in front of every round left the
+                // streaming kernels at half the resident kernels' rate: C4's 64 KiB - 1 MiB list)
+                uint4 q[PF];
+#pragma unroll
+                for (int k = 0; k < PF; ++k) q[k] = live((uint32_t)k) ? load_group(gw0 + k * 64 + lane) : uint4{};
+                bool go = true;
+                for (uint32_t r0 = 0; go; r0 += PF) {
+#pragma unroll
+                    for (int k = 0; k < PF; ++k) {
+                        const uint32_t r = r0 + (uint32_t)k;
+                        if (!live(r)) {
+                            go = false;
+                            break;
+                        }
+                        uint4 d = q[k];
+                        if (live(r + PF)) q[k] = load_group(gw0 + (r + PF) * 64 + lane);
+                        uint32_t c = 0;
+                        body(r, d, c, std::false_type{});
+                    }
+                }
             }
         }
     };
