@@ -242,13 +242,13 @@ bool policy_on(const tdt_ctx *c) {
            c->bandwidth.load() < c->cfg.bandwidth_threshold_mbps;
 }
 
-template <int WS, int TEAM, int G, int MODE, int LB>
+template <int WS, int TEAM, int G, int MODE, int LB, int PATH = psy::PATH_BOTH>
 int launch_encode_t(psy::EncodeArgs a, hipStream_t s) {
     // one workgroup per message; a launch holds < 2^32 threads, so very large batches take
     // several (message ids come from the ticket, so the look-back order spans them)
     const uint32_t maxb = 0xffffffffu / TEAM;
     for (uint32_t b = 0; b < a.n_msgs; b += maxb)
-        hipLaunchKernelGGL((psy::tdt_encode_kernel<WS, TEAM, G, MODE, LB>), dim3(std::min(maxb, a.n_msgs - b)),
+        hipLaunchKernelGGL((psy::tdt_encode_kernel<WS, TEAM, G, MODE, LB, 0, 0, PATH>), dim3(std::min(maxb, a.n_msgs - b)),
                            dim3(TEAM), 0, s, a);
     return TDT_OK;
 }
@@ -647,9 +647,14 @@ int launch_slotted_any(tdt_ctx *c, PlanWS &pw, psy::EncodeArgs a, hipStream_t s)
 #define PSY_BIG_G 8
 #endif
 
+// res: every message is aligned, a whole number of 16-byte groups and at most 64 KiB (the
+// caller checked): the resident-only kernel (without the streaming body's live registers; the
+// one-pass compacted C3 encode 9.58 ms with both bodies)
 template <int WS, int MODE, int LB>
-int launch_encode_ws(psy::EncodeArgs a, bool small, hipStream_t s) {
+int launch_encode_ws(psy::EncodeArgs a, bool small, bool res, hipStream_t s) {
     if (small) return launch_encode_t<WS, 64, 4, MODE, LB>(a, s);
+    if constexpr (MODE == psy::MODE_ENCODE && LB == 1 && PSY_BIG_TEAM == 512 && PSY_BIG_G == 8)
+        if (res) return launch_encode_t<WS, 512, 8, MODE, LB, psy::PATH_RES>(a, s);
     return launch_encode_t<WS, PSY_BIG_TEAM, PSY_BIG_G, MODE, LB>(a, s);
 }
 
@@ -664,18 +669,21 @@ bool lb_small_teams(tdt_ctx *c, hipStream_t s) {
     return c->size_hint.load() <= kSmallMax;
 }
 
+// small_teams: -1 from the context's history, 0 message-sized teams, 1 one-wave teams, 2
+// message-sized resident-only teams (see launch_encode_ws)
 template <int MODE, int LB>
 int launch_encode(tdt_ctx *c, psy::EncodeArgs a, hipStream_t s, int small_teams) {
-    const bool small = small_teams < 0 ? lb_small_teams(c, s) : small_teams != 0;
+    const bool small = small_teams < 0 ? lb_small_teams(c, s) : small_teams == 1;
+    const bool res = small_teams == 2;
     switch (c->cfg.word_size) {
 #ifdef PSY_FAST_BUILD  // diagnostic builds: word_size 4 only
-        case 4: return launch_encode_ws<4, MODE, LB>(a, small, s);
+        case 4: return launch_encode_ws<4, MODE, LB>(a, small, res, s);
 #else
-        case 1: return launch_encode_ws<1, MODE, LB>(a, small, s);
-        case 2: return launch_encode_ws<2, MODE, LB>(a, small, s);
-        case 4: return launch_encode_ws<4, MODE, LB>(a, small, s);
-        case 8: return launch_encode_ws<8, MODE, LB>(a, small, s);
-        case 16: return launch_encode_ws<16, MODE, LB>(a, small, s);
+        case 1: return launch_encode_ws<1, MODE, LB>(a, small, res, s);
+        case 2: return launch_encode_ws<2, MODE, LB>(a, small, res, s);
+        case 4: return launch_encode_ws<4, MODE, LB>(a, small, res, s);
+        case 8: return launch_encode_ws<8, MODE, LB>(a, small, res, s);
+        case 16: return launch_encode_ws<16, MODE, LB>(a, small, res, s);
 #endif
     }
     return set_err(TDT_E_UNSUPPORTED, "word_size not supported on the GPU path");
@@ -1630,10 +1638,18 @@ int host_path(tdt_ctx *c, bool encode, const uint8_t *h_in, const uint64_t *h_in
 
 namespace {
 // any message longer than `lim` bytes → *flag = 1 (one atomic per workgroup)
-__global__ __launch_bounds__(256) void cp_big_kernel(const uint64_t *in_off, uint32_t n, uint64_t lim, uint64_t *flag) {
+// any message longer than `lim` bytes → *flag |= 1; any message that the resident-only kernel
+// cannot hold (unaligned start, a partial 16-byte group, over 64 KiB) → *flag |= 2 (one atomic
+// per workgroup and bit)
+__global__ __launch_bounds__(256) void cp_big_kernel(const uint8_t *in, const uint64_t *in_off, uint32_t n,
+                                                     uint64_t lim, uint64_t *flag) {
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-    const bool big = i < n && in_off[i + 1] - in_off[i] > lim;
-    if (__syncthreads_or(big) && threadIdx.x == 0) atomicOr(reinterpret_cast<unsigned long long *>(flag), 1ull);
+    const uint64_t len = i < n ? in_off[i + 1] - in_off[i] : 0;
+    const bool big = i < n && len > lim;
+    const bool nonres = i < n && (len > 65536 || (len & 15) != 0 || (((uintptr_t)in + in_off[i]) & 15) != 0);
+    const bool any_big = __syncthreads_or(big), any_nonres = __syncthreads_or(nonres);
+    if (threadIdx.x == 0 && (any_big || any_nonres))
+        atomicOr(reinterpret_cast<unsigned long long *>(flag), (any_big ? 1ull : 0ull) | (any_nonres ? 2ull : 0ull));
 }
 // lengths → the scan's input (in place in out_off)
 __global__ __launch_bounds__(256) void cp_len_kernel(const uint64_t *len, uint64_t *out_off, uint32_t n) {
@@ -1823,7 +1839,7 @@ int tdt_encode_batch(tdt_ctx *ctx, const uint8_t *d_in, const uint64_t *d_in_off
         }
         uint64_t *flag = ctx->cp_idx + 2ull * n_msgs + 1;
         HIPCHK(hipMemsetAsync(flag, 0, 8, s));
-        hipLaunchKernelGGL(cp_big_kernel, dim3((n_msgs + 255) / 256), dim3(256), 0, s, d_in_off, n_msgs,
+        hipLaunchKernelGGL(cp_big_kernel, dim3((n_msgs + 255) / 256), dim3(256), 0, s, d_in, d_in_off, n_msgs,
                            (uint64_t)65536, flag);
         HIPCHK(hipGetLastError());
         HIPCHK(hipMemcpyAsync(&h3[0], flag, 8, hipMemcpyDeviceToHost, s));
@@ -1834,9 +1850,10 @@ int tdt_encode_batch(tdt_ctx *ctx, const uint8_t *d_in, const uint64_t *d_in_off
     // one pass with the look-back for batches of medium messages (all <= 64 KiB, 16 KiB or more
     // on average); small messages make the per-message ticket and look-back chain the limit
     // (C2: 12 ms for 1 Mi x 1 KiB), long ones stall it — both take the two phases
-    if (!h3[0] && (h3[2] - h3[1]) >= 16384ull * n_msgs)  // (16 KiB on average: 512-lane teams)
+    if (!(h3[0] & 1) && (h3[2] - h3[1]) >= 16384ull * n_msgs)  // (16 KiB on average: 512-lane teams)
         return encode_common(ctx, psy::MODE_ENCODE, d_in, d_in_off, n_msgs, nullptr, d_out, out_cap, d_out_off,
-                             d_status, nullptr, nullptr, nullptr, stream, nullptr, nullptr, nullptr, nullptr, 0);
+                             d_status, nullptr, nullptr, nullptr, stream, nullptr, nullptr, nullptr, nullptr,
+                             (h3[0] & 2) ? 0 : 2);
     uint64_t *slot = ctx->cp_idx, *len = ctx->cp_idx + n_msgs + 1;
     // Σ encode bounds <= 2·(input bytes) + n·(28 + 4·ws) (and >= n + 4 per message)
     const uint64_t bound = 2 * (h3[2] - h3[1]) + (uint64_t)n_msgs * (28 + 4ull * (uint64_t)ctx->cfg.word_size + 4);

@@ -2239,6 +2239,6 @@ __global__ __launch_bounds__(64) void tdt_encode_lscan_kernel(EncodeArgs a, cons
     X(WS, 512, 8, MODE_ENCODE, 0, 4, 1, 0) X(WS, 64, 4, MODE_ENCODE, 0, 0, 1, 0) X(WS, 256, 8, MODE_ENCODE, 0, 0, 0, 0)  \
     X(WS, 256, 8, MODE_ENCODE, 0, 0, 1, 0) X(WS, 64, 4, MODE_ENCODE, 1, 0, 0, 0) X(WS, 512, 8, MODE_ENCODE, 1, 0, 0, 0)  \
     X(WS, 64, 4, MODE_MAPPED, 1, 0, 0, 0) X(WS, 512, 8, MODE_MAPPED, 1, 0, 0, 0) X(WS, 64, 4, MODE_ANALYZE, 1, 0, 0, 0)  \
-    X(WS, 512, 8, MODE_ANALYZE, 1, 0, 0, 0)
+    X(WS, 512, 8, MODE_ANALYZE, 1, 0, 0, 0) X(WS, 512, 8, MODE_ENCODE, 1, 0, 0, 1)
 
 }  // namespace psy

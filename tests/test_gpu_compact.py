@@ -152,3 +152,40 @@ def test_compacted_under_graph_capture():
     assert np.array_equal(eoff.cpu().numpy(), roff.cpu().numpy())
     n = int(roff[-1].item())
     assert np.array_equal(out[:n].cpu().numpy(), ref[:n].cpu().numpy())
+
+
+@pytest.mark.parametrize("variant", ["resident", "odd_size", "unaligned"])
+def test_lookback_resident_only_kernel(variant):
+    """Batches of 16-64 KiB messages take the one-pass look-back kernel; when every message is
+    aligned, whole 16-byte groups and at most 64 KiB (checked on the device before the launch)
+    it is the resident-only instance, otherwise the one with both bodies.  Either way every blob
+    equals the oracle's, the offsets are the blob sizes' prefix sums, and the batch decodes
+    back."""
+    rng = np.random.default_rng({"resident": 11, "odd_size": 12, "unaligned": 13}[variant])
+    sizes = list(rng.integers(1024, 4097, 240) * 16)
+    if variant == "odd_size":
+        sizes[100] += 4  # a partial 16-byte group
+    msgs = [_gradient(rng, int(s)) for s in sizes]
+    lead = 4 if variant == "unaligned" else 0
+    off = np.zeros(len(msgs) + 1, np.int64)
+    off[0] = lead
+    off[1:] = lead + np.cumsum([m.size for m in msgs])
+    data = np.zeros(int(off[-1]), np.uint8)
+    for i, m in enumerate(msgs):
+        data[off[i]:off[i + 1]] = m
+    codec = _codec()
+    d = torch.from_numpy(data).cuda()
+    o = torch.from_numpy(off).cuda()
+    out, eoff, st = codec.encode_batch(d, o)
+    torch.cuda.synchronize()
+    b, eo, s = out.cpu().numpy(), eoff.cpu().numpy(), st.cpu().numpy()
+    assert (s == 0).all()
+    assert codec.error_flags() == 0
+    orc = Oracle()
+    cfg = orc.config(sample_fraction=1.0)
+    for i, m in enumerate(msgs):
+        assert bytes(b[eo[i]:eo[i + 1]]) == bytes(orc.encode(m, cfg=cfg, bandwidth=10.0)), i
+    back, doff, dst = codec.decode_batch(torch.from_numpy(b[:eo[-1]].copy()).cuda(), torch.from_numpy(eo).cuda())
+    torch.cuda.synchronize()
+    assert int(dst.abs().sum()) == 0
+    assert np.array_equal(back.cpu().numpy()[: off[-1] - off[0]], data[lead:])
