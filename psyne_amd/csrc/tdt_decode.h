@@ -184,7 +184,30 @@ __global__ __launch_bounds__(256) void tdt_decode_sizes_kernel(DecodeArgs a) {
     const uint64_t len = a.in_len ? a.in_len[msg] : a.in_off[msg + 1] - boff;
     const uint8_t *blob = a.in + boff;
     const bool al4 = ((uintptr_t)blob & 3) == 0;
+    // the first 48 bytes (header, a word-size-4 mapping, the first stream's length) in one burst
+    // of independent loads: the header check then waits on memory once more at most (the second
+    // stream's length), instead of once per field
+    uint32_t w[12];
+    const bool pre = al4 && len >= 48;
+    if (pre) {
+        if (((uintptr_t)blob & 15) == 0) {
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                const uint4 v = *reinterpret_cast<const uint4 *>(blob + 16 * q);
+                w[4 * q] = v.x, w[4 * q + 1] = v.y, w[4 * q + 2] = v.z, w[4 * q + 3] = v.w;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 12; ++k) w[k] = *reinterpret_cast<const uint32_t *>(blob + 4 * k);
+        }
+    }
     auto rd32 = [&](uint64_t off) -> uint32_t {
+        if (pre && off < 48 && (off & 3) == 0) {
+            uint32_t v = w[0];
+#pragma unroll
+            for (int k = 1; k < 12; ++k) v = (off >> 2) == (uint64_t)k ? w[k] : v;
+            return v;
+        }
         return (al4 && (off & 3) == 0) ? *reinterpret_cast<const uint32_t *>(blob + off) : ld_u32_bytes(blob + off);
     };
     uint32_t uncp;
@@ -1138,9 +1161,19 @@ __global__ __launch_bounds__(1024) void tdt_decode_plan_kernel(DPlanArgs p) {
             const uint64_t len = p.in_len ? p.in_len[i] : p.in_off[i + 1] - boff;
             uint64_t osz = 0, nbs = 0;
             if (len >= 20) {
-                const uint32_t magic = ld_u32_bytes(p.in + boff);
+                const uint8_t *bp = p.in + boff;
+                const bool al8 = ((uintptr_t)bp & 7) == 0;
+                uint32_t magic, w1;
+                if (al8) {  // (one 8-byte load instead of eight byte loads)
+                    const uint2 v = *reinterpret_cast<const uint2 *>(bp);
+                    magic = v.x;
+                    w1 = v.y;
+                } else {
+                    magic = ld_u32_bytes(bp);
+                    w1 = ld_u32_bytes(bp + 4);
+                }
                 if (magic == kMagicTDT) {
-                    osz = ld_u32_bytes(p.in + boff + 4);
+                    osz = w1;
                     nbs = len / 1024 + 3;  // >= the 512-pair blocks of <= 2 referenced streams
                 } else if (magic == kMagicUNCP) {
                     osz = len - 4;
