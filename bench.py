@@ -347,6 +347,28 @@ def cpu_baseline(data_u8, msg_bytes, target_s, threads, kind):
                 affinity_mask=aff)
 
 
+def copy_ceiling(torch, dev, nbytes=2 << 30, reps=5):
+    """Achievable HBM rate of a plain device-to-device copy on this box (the
+    "achievable stream-copy ceiling" beside the 8 TB/s peak): torch copy_ between two device
+    buffers, HIP events around `reps` copies, read + write bytes counted."""
+    a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    b = torch.empty_like(a)
+    a.fill_(1)
+    b.copy_(a)
+    b.copy_(a)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    stream = torch.cuda.current_stream(dev)
+    ev[0].record(stream)
+    for _ in range(reps):
+        b.copy_(a)
+    ev[1].record(stream)
+    torch.cuda.synchronize(dev)
+    t = ev[0].elapsed_time(ev[1]) / reps * 1e-3
+    del a, b
+    return {"GBps": round(2 * nbytes / t / 1e9, 1), "bytes_copied": nbytes,
+            "note": "device-to-device torch copy_, read + write bytes / HIP-event time, %d reps" % reps}
+
+
 def pcie_ceiling(torch, dev, nbytes=256 << 20, reps=5):
     """Pinned hipMemcpyAsync ceilings (GB/s): H2D alone, D2H alone, and both directions at once
     on two streams — the bound of the host-inclusive pipeline."""
@@ -673,6 +695,7 @@ def main():
         sha = lib_sha256()
         tr = load_traffic(key, sha)
         traffic = tr["kernels"][dom].get("hbm_bytes_per_launch") if tr and dom in tr.get("kernels", {}) else None
+        ceil = copy_ceiling(torch, dev)  # (after the timed region; rank 0)
         cpu = None
         if a.cpu_seconds > 0 and a.workload == "c3" and world == 1:  # rank 0 at N=1 only
             if orig_affinity:
@@ -720,6 +743,7 @@ def main():
                          "traffic_source": tr["_file"] if traffic is not None else
                          "no PMC record for this library build (lib sha256 %s)" % sha[:16],
                          "algorithmic_bytes_per_launch": alg,
+                         "copy_ceiling": ceil, "frac_of_copy_ceiling": round(achieved / ceil["GBps"], 4),
                          "combined": {"achieved": round(combined, 2), "frac": round(combined / HBM_PEAK_GBS, 4),
                                       "def": "2(n+E) / (t_enc + t_dec), SURVEY.md 8(d)"}},
             "kernels_ms": {"encode": round(t_enc, 4), "decode": round(t_dec, 4)},
