@@ -854,10 +854,11 @@ private:
             rx_max_msg_ = std::max<uint64_t>(rx_max_msg_, max_msg);
         }
         if (!rx_thread_.joinable()) {
-            // the read-ahead ring pinned up front (frames and payloads of a full buffer at a
-            // 1.5x decoded/wire ratio; larger payloads grow a buffer once)
+            // the read-ahead ring, plus two buffers for the views a consumer holds, pinned up
+            // front (frames and payloads of a full buffer at a 1.5x decoded/wire ratio; larger
+            // payloads grow a buffer once): pinning one mid-run stalled the receiver for ~8 ms
             const uint64_t fcap = frame_capacity(max_msg);
-            while (rx_pool_.size() < kRing + 1) {
+            while (rx_pool_.size() < kRing + 3) {
                 rx_pool_.push_back(std::make_unique<RxBuf>());
                 rx_pool_.back()->mem.reserve(std::max<uint64_t>(kRxBytes + fcap, 2 * fcap));
                 rx_pool_.back()->dec.reserve(kRxBytes + kRxBytes / 2);

@@ -153,6 +153,7 @@ struct tdt_ctx {
     // device buffers a captured graph may still reference after a growth (ws, slot_sums): freed
     // at tdt_ctx_destroy, never while the context lives
     std::vector<void *> retired;
+    std::vector<void *> retired_host;  // pinned host-pipeline buffers replaced by larger ones
     size_t ws_bytes = 0;
     // per-chunk sums of tdt_decode_slots' two-pass scan (one u64 per 8192 messages; stream-ordered
     // like `ws`: one slotted decode per context at a time)
@@ -983,15 +984,17 @@ int ensure_slot(tdt_ctx *c, int k, size_t dev_bytes, size_t pin_words, size_t si
         HIPCHK(hipHostMalloc(&h.flag, 4, hipHostMallocDefault));
         *h.flag = 0;
     }
-    // growth takes 1.5x (whole MiB): a hipFree waits for the whole device (every stream, other
-    // contexts' too) and pinning host memory costs milliseconds, so buffers sized by the chunks
-    // of varying calls should settle after a few
+    // growth takes 1.5x (whole MiB) and retires the old buffer until tdt_ctx_destroy instead of
+    // freeing it: a hipFree waits for the whole device (every stream, the other contexts' of
+    // the process too: a C1 loopback end stalled the other end's pipeline for milliseconds), and
+    // pinning host memory costs milliseconds, so buffers sized by the chunks of varying calls
+    // settle after a few (the retired ones sum to less than twice the last)
     auto grown = [](size_t need, size_t have) {
         return (std::max(need, have + have / 2) + (1u << 20) - 1) & ~size_t((1u << 20) - 1);
     };
     if (dev_bytes > h.dev_bytes) {
         const size_t cap = grown(dev_bytes, h.dev_bytes);
-        if (h.dev) HIPCHK(hipFree(h.dev));
+        if (h.dev) c->retired.push_back(h.dev);  // (the slot's earlier chunks are done: synced)
         h.dev = nullptr;
         h.dev_bytes = 0;
         HIPCHK(hipMalloc(&h.dev, cap));
@@ -1000,7 +1003,7 @@ int ensure_slot(tdt_ctx *c, int k, size_t dev_bytes, size_t pin_words, size_t si
     auto pinned = [&](uint8_t *&buf, size_t &have, size_t need) -> int {
         if (need <= have) return TDT_OK;
         const size_t cap = grown(need, have);
-        if (buf) HIPCHK(hipHostFree(buf));
+        if (buf) c->retired_host.push_back(buf);
         buf = nullptr;
         have = 0;
         HIPCHK(hipHostMalloc(&buf, cap, hipHostMallocDefault));
@@ -1742,6 +1745,7 @@ void tdt_ctx_destroy(tdt_ctx *ctx) {
     if (ctx->cp_buf) (void)hipFree(ctx->cp_buf);
     if (ctx->cp_idx) (void)hipFree(ctx->cp_idx);
     for (void *p : ctx->retired) (void)hipFree(p);
+    for (void *p : ctx->retired_host) (void)hipHostFree(p);
     ctx->pw.release();
     if (ctx->hbases) (void)hipFree(ctx->hbases);
     if (ctx->one_stream) (void)hipStreamSynchronize(ctx->one_stream);
