@@ -26,9 +26,15 @@
 // from the first send to the last verified receive (the reference's "Effective throughput ...
 // MB/s (original)", :401-403), after an untimed warm-up pass of --warm batches (default 2: the
 // first calls of each end allocate its workspaces and pinned staging).  --mem pinned puts the
-// tensors in pinned host memory (as a channel's message buffers could be) for every row.  One
-// JSON line on stdout.
+// tensors in pinned host memory (as a channel's message buffers could be) for every row.
+// --procs 2 runs the receiving end in a child process forked before anything touches the GPU, so
+// each end has its own process, HIP context and hardware queues, as the two hosts' ends of a link
+// would (they still share this host's GPU, PCIe link and cores); the child reports its end time
+// (CLOCK_MONOTONIC, shared by both processes) and its mismatch count through a pipe.  One JSON line
+// on stdout.
 #include <dlfcn.h>
+#include <sys/wait.h>
+#include <unistd.h>
 
 #include <psyne_amd/tdt_substrate.hpp>
 
@@ -83,7 +89,7 @@ int main(int argc, char **argv) {
     // the tensors' memory, for every row: "pageable" (std::vector, default) or "pinned"
     // (tdt_host_alloc: the GPU row's encode DMAs them directly instead of staging them)
     std::string mem = "pageable";
-    int port = 18080;
+    int port = 18080, procs = 1;
     std::string codec = "gpu", dump;
     for (int i = 1; i + 1 < argc; i += 2) {
         const std::string k = argv[i], v = argv[i + 1];
@@ -97,6 +103,30 @@ int main(int argc, char **argv) {
         else if (k == "--half") half = v;
         else if (k == "--rx") rxmode = v;
         else if (k == "--mem") mem = v;
+        else if (k == "--procs") procs = std::stoi(v);
+    }
+    // --procs 2: fork before any thread exists and before anything touches the GPU (pinned
+    // payloads included); role "tx" = the parent (sender), "rx" = the child (receiver)
+    std::string role = "both";
+    int rep[2] = {-1, -1};
+    pid_t child = -1;
+    if (procs == 2) {
+        if (half != "both") {
+            std::fprintf(stderr, "--procs 2 runs both halves (no --half)\n");
+            return 2;
+        }
+        if (::pipe(rep) != 0) {
+            std::perror("pipe");
+            return 2;
+        }
+        std::fflush(nullptr);
+        child = ::fork();
+        if (child < 0) {
+            std::perror("fork");
+            return 2;
+        }
+        role = child == 0 ? "rx" : "tx";
+        ::close(child == 0 ? rep[0] : rep[1]);
     }
     const size_t bytes = floats * 4;
     // payloads (GRADIENTS: 70 % zeros, N(0, 0.01) otherwise)
@@ -125,19 +155,26 @@ int main(int argc, char **argv) {
 
     std::unique_ptr<PosixTcpSubstrate> raw_rx, raw_tx;
     std::unique_ptr<TdtSubstrate<PosixTcpSubstrate>> rx, tx;
-    PosixTcpSubstrate *rx_inner, *tx_inner;
+    PosixTcpSubstrate *rx_inner = nullptr, *tx_inner = nullptr;
+    const bool has_rx = role != "tx", has_tx = role != "rx";
     if (codec == "gpu") {
-        rx = std::make_unique<TdtSubstrate<PosixTcpSubstrate>>(cfg, "127.0.0.1", (uint16_t)port, true);
-        tx = std::make_unique<TdtSubstrate<PosixTcpSubstrate>>(cfg, "127.0.0.1", (uint16_t)port, false);
-        rx_inner = &rx->inner();
-        tx_inner = &tx->inner();
+        if (has_rx) {
+            rx = std::make_unique<TdtSubstrate<PosixTcpSubstrate>>(cfg, "127.0.0.1", (uint16_t)port, true);
+            rx_inner = &rx->inner();
+        }
+        if (has_tx) {
+            tx = std::make_unique<TdtSubstrate<PosixTcpSubstrate>>(cfg, "127.0.0.1", (uint16_t)port, false);
+            tx_inner = &tx->inner();
+        }
     } else {
-        raw_rx = std::make_unique<PosixTcpSubstrate>("127.0.0.1", (uint16_t)port, true);
-        raw_tx = std::make_unique<PosixTcpSubstrate>("127.0.0.1", (uint16_t)port, false);
+        if (has_rx) raw_rx = std::make_unique<PosixTcpSubstrate>("127.0.0.1", (uint16_t)port, true);
+        if (has_tx) raw_tx = std::make_unique<PosixTcpSubstrate>("127.0.0.1", (uint16_t)port, false);
         rx_inner = raw_rx.get();
         tx_inner = raw_tx.get();
     }
-    if (!rx_inner->wait_for_connection() || !tx_inner->wait_for_connection()) {
+    // (two processes: the other end may still be generating its payloads or starting its GPU)
+    const std::chrono::milliseconds cwait(procs == 2 ? 60000 : 5000);
+    if ((rx_inner && !rx_inner->wait_for_connection(cwait)) || (tx_inner && !tx_inner->wait_for_connection(cwait))) {
         std::fprintf(stderr, "connection failed\n");
         return 2;
     }
@@ -152,7 +189,7 @@ int main(int argc, char **argv) {
         ref_rx = ref.make(1.0f, 4, 10.0);
     }
     FILE *frames = nullptr;
-    if (!dump.empty()) {
+    if (!dump.empty() && has_tx) {
         FILE *f = std::fopen((dump + "/inputs.bin").c_str(), "wb");
         for (auto &m : msgs) std::fwrite(m.data(), 1, bytes, f);
         std::fclose(f);
@@ -187,8 +224,8 @@ int main(int argc, char **argv) {
     // One pass: tensors [0, n) sent in batches and verified on receipt.  The warm-up pass (not
     // timed: context workspaces, pinned staging and plan histories are set up by the first calls
     // of each end) precedes the timed pass over all `count` tensors.
-    auto pass = [&](size_t n, FILE *frames) {
-    std::thread receiver([&] {
+    // the receiving end's part of a pass over tensors [0, n)
+    auto recv_part = [&](size_t n) {
         std::vector<uint8_t> out;
         std::vector<uint64_t> off;
         std::vector<uint8_t> frame(tdt_encode_bound(bytes, 4) + 64), back(bytes);
@@ -234,7 +271,9 @@ int main(int argc, char **argv) {
                 if (glen != bytes || std::memcmp(got, msgs[b + i].data(), bytes)) ++mismatches;
             }
         }
-    });
+    };
+    // the sending end's part
+    auto send_part = [&](size_t n, FILE *frames) {
     if (codec == "gpu") tx->record_last_batch(frames != nullptr || half == "rx");
     for (size_t b = 0; b < n; b += batch) {
         const size_t nb = std::min(batch, n - b);
@@ -279,7 +318,36 @@ int main(int argc, char **argv) {
         }
     }
     if (codec == "gpu" && half != "rx") tx->flush();  // every queued frame is on the wire
-    receiver.join();
+    };
+    auto pass = [&](size_t n, FILE *frames) {
+        if (!has_tx) return recv_part(n);
+        if (!has_rx) return send_part(n, frames);
+        std::thread receiver([&] { recv_part(n); });
+        send_part(n, frames);
+        receiver.join();
+    };
+    // child → parent reports (--procs 2)
+    struct Report {
+        int64_t t_ns;  // CLOCK_MONOTONIC (steady_clock) time of the report
+        uint64_t mismatches;
+    };
+    auto now_ns = [] {
+        return (int64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                   std::chrono::steady_clock::now().time_since_epoch())
+            .count();
+    };
+    auto send_report = [&] {
+        const Report r{now_ns(), (uint64_t)mismatches};
+        return ::write(rep[1], &r, sizeof(r)) == (ssize_t)sizeof(r);
+    };
+    auto read_report = [&](Report &r) {
+        size_t got = 0;
+        while (got < sizeof(r)) {
+            const ssize_t k = ::read(rep[0], reinterpret_cast<char *>(&r) + got, sizeof(r) - got);
+            if (k <= 0) return false;
+            got += (size_t)k;
+        }
+        return true;
     };
     if (warm) {
         pass(std::min(count, warm * batch), nullptr);
@@ -288,12 +356,54 @@ int main(int argc, char **argv) {
     using PS = TdtSubstrate<PosixTcpSubstrate>::PipeStats;
     PS tx0{}, rx0{};
     if (codec == "gpu") {
-        tx0 = tx->pipe_stats();
-        rx0 = rx->pipe_stats();
+        if (tx) tx0 = tx->pipe_stats();
+        if (rx) rx0 = rx->pipe_stats();
+    }
+    if (role == "rx") {
+        // warm-up done (the parent starts its clock on this report), then the timed pass
+        if (!send_report()) return 6;
+        pass(count, nullptr);
+        const bool ok = send_report();
+        if (codec == "gpu") {
+            const PS r = rx->pipe_stats();
+            std::fprintf(stderr,
+                         "{\"pipe_rx\": {\"recv\": %.4f, \"rx_sleep\": %.4f, \"rx_wait\": %.4f, \"decode\": %.4f, "
+                         "\"decode_calls\": %llu, \"decode_MB\": %.1f, \"dec_wait\": %.4f, \"deliver_wait\": %.4f}}\n",
+                         r.recv - rx0.recv, r.rx_sleep - rx0.rx_sleep, r.rx_wait - rx0.rx_wait, r.decode - rx0.decode,
+                         (unsigned long long)(r.decode_calls - rx0.decode_calls),
+                         double(r.decode_bytes - rx0.decode_bytes) / 1e6, r.dec_wait - rx0.dec_wait,
+                         r.deliver_wait - rx0.deliver_wait);
+        }
+        ::close(rep[1]);
+        return !ok ? 6 : mismatches ? 1 : 0;
+    }
+    Report rr{};
+    auto reap = [&]() -> int {  // the child's exit code (-1: abnormal)
+        int ws = 0;
+        if (::waitpid(child, &ws, 0) != child || !WIFEXITED(ws)) return -1;
+        return WEXITSTATUS(ws);
+    };
+    if (role == "tx" && !read_report(rr)) {
+        std::fprintf(stderr, "receiver process ended during the warm-up (exit %d)\n", reap());
+        return 6;
     }
     const auto t0 = std::chrono::steady_clock::now();
     pass(count, frames);
-    const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (role == "tx") {
+        // the receiving end's last verified receive ends the clock
+        if (!read_report(rr)) {
+            std::fprintf(stderr, "receiver process ended without its report (exit %d)\n", reap());
+            return 6;
+        }
+        secs = (double)(rr.t_ns - std::chrono::duration_cast<std::chrono::nanoseconds>(t0.time_since_epoch()).count()) * 1e-9;
+        mismatches = (size_t)rr.mismatches;
+        const int code = reap();
+        if (code != 0 && code != 1) {
+            std::fprintf(stderr, "receiver process exit %d\n", code);
+            return 6;
+        }
+    }
     if (frames) std::fclose(frames);
     if (ref_tx) ref.release(ref_tx);
     if (ref_rx) ref.release(ref_rx);
@@ -301,12 +411,19 @@ int main(int argc, char **argv) {
     std::printf("{\"harness\": \"tcp_loopback\", \"codec\": \"%s\", \"tensors\": %zu, \"tensor_bytes\": %zu, "
                 "\"batch\": %zu, \"seconds\": %.4f, \"original_MB\": %.1f, \"wire_MB\": %.1f, "
                 "\"compression_ratio\": %.4f, \"effective_MBps\": %.1f, \"network_MBps\": %.1f, "
-                "\"mismatches\": %zu, \"warmup_tensors\": %zu, \"half\": \"%s\", \"rx\": \"%s\", \"mem\": \"%s\"}\n",
+                "\"mismatches\": %zu, \"warmup_tensors\": %zu, \"half\": \"%s\", \"rx\": \"%s\", \"mem\": \"%s\", "
+                "\"procs\": %d}\n",
                 codec.c_str(), count, bytes, codec == "gpu" ? batch : (size_t)1, secs, orig / 1e6,
                 double(wire) / 1e6, orig / double(wire), orig / 1e6 / secs, double(wire) / 1e6 / secs, mismatches,
                 warm ? std::min(count, warm * batch) : (size_t)0, half.c_str(), codec == "gpu" ? rxmode.c_str() : "-",
-                mem.c_str());
-    if (codec == "gpu") {
+                mem.c_str(), procs == 2 ? 2 : 1);
+    if (codec == "gpu" && role == "tx") {
+        const PS t = tx->pipe_stats();
+        std::fprintf(stderr,
+                     "{\"pipe_tx\": {\"encode\": %.4f, \"encode_calls\": %llu, \"tx_wait\": %.4f, \"send\": %.4f}}\n",
+                     t.encode - tx0.encode, (unsigned long long)(t.encode_calls - tx0.encode_calls), t.tx_wait - tx0.tx_wait,
+                     t.send - tx0.send);
+    } else if (codec == "gpu") {
         // where the pipeline threads spent the timed pass (seconds)
         const PS t = tx->pipe_stats(), r = rx->pipe_stats();
         std::fprintf(stderr,

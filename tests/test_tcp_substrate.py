@@ -51,6 +51,15 @@ def test_framing_passthrough_loopback():
     assert abs(r["compression_ratio"] - 1.0) < 1e-9
 
 
+def test_framing_passthrough_two_processes():
+    # --procs 2: the receiving end in a forked child (its own process, as the far host's end would
+    # be); the child's end time and mismatch count come back through a pipe
+    r = run("--codec", "none", "--count", "64", "--floats", "16384", "--batch", "8", "--port", "18185",
+            "--procs", "2")
+    assert r["mismatches"] == 0 and r["tensors"] == 64 and r["procs"] == 2
+    assert r["seconds"] > 0
+
+
 def test_reference_codec_loopback(tmp_path):
     # psyne's own CPU path (the compiled reference protocol) over the same frames; its wire
     # blobs are the oracle's (the oracle is pinned against this library)
@@ -85,6 +94,17 @@ def test_tdt_substrate_gpu_loopback_c1_workload(tmp_path):
     assert r["mismatches"] == 0 and r["tensors"] == 1000
     assert r["compression_ratio"] > 1.2
     check_frames_vs_oracle(tmp_path, 1000, 256 * 1024)
+
+
+@pytest.mark.gpu
+def test_tdt_substrate_gpu_loopback_two_processes(tmp_path):
+    # each end in its own process with its own GPU codec context (forked before either touches
+    # the GPU); every payload verified by the child, every wire frame against the oracle
+    r = run("--codec", "gpu", "--count", "40", "--floats", "65536", "--batch", "8", "--port", "18186",
+            "--procs", "2", "--dump", str(tmp_path))
+    assert r["mismatches"] == 0 and r["procs"] == 2
+    assert r["compression_ratio"] > 1.1
+    check_frames_vs_oracle(tmp_path, 40, 65536)
 
 
 @pytest.mark.gpu
