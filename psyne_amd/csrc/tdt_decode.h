@@ -488,7 +488,7 @@ __device__ __forceinline__ void decode_fast(const FastHdr &H, uint8_t *smem, con
             if (dal16 && 16ull * (g0 + 64u) <= wbytes) {
                 // a whole aligned round (uniform): one 16-byte store per lane, no per-lane tests
 #ifndef PSY_X_NOSTORE
-                *reinterpret_cast<uint4 *>(dst + 16ull * g) = o;
+                st16_nt(dst + 16ull * g, o);
 #else
                 if (o.x == 0x12345678u && o.y == 0x9abcdef0u) *reinterpret_cast<uint4 *>(dst + 16ull * g) = o;
 #endif

@@ -289,6 +289,9 @@ constexpr uint32_t kRecount = 0xffffffffu;
 // 4 chunk bits of the wave's first group (combined slot layout)
 
 typedef uint32_t u32_a2 __attribute__((aligned(2)));  // a dword stored at a 2-byte aligned address
+__device__ __forceinline__ void st32a2_nt(uint8_t *p, uint32_t v) {  // (non-temporal: tdt_device.h st16_nt)
+    __builtin_nontemporal_store(v, (__attribute__((address_space(1))) u32_a2 *)(p));
+}
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t popc(uint32_t x) { return (uint32_t)__builtin_popcount(x); }
 __device__ __forceinline__ uint32_t hibit(uint32_t x) { return 31u - (uint32_t)__builtin_clz(x); }
@@ -1744,15 +1747,15 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
                     for (; k0 + 256u <= K; k0 += 256u) {
                         const uint32_t k = k0 + 2u * (uint32_t)lane;
                         const uint32_t pa = pairs2_at(k), pb = pairs2_at(k + 128u);
-                        *reinterpret_cast<u32_a2 *>(Dp + 2u * k) = pa;
-                        *reinterpret_cast<u32_a2 *>(Dp + 2u * k + 256u) = pb;
+                        st32a2_nt(Dp + 2u * k, pa);
+                        st32a2_nt(Dp + 2u * k + 256u, pb);
                     }
                     for (; k0 + 128u <= K; k0 += 128u) {
                         const uint32_t k = k0 + 2u * (uint32_t)lane;
-                        *reinterpret_cast<u32_a2 *>(Dp + 2u * k) = pairs2_at(k);
+                        st32a2_nt(Dp + 2u * k, pairs2_at(k));
                     }
                     const uint32_t k = k0 + 2u * (uint32_t)lane;
-                    if (k + 1u < K) *reinterpret_cast<u32_a2 *>(Dp + 2u * k) = pairs2_at(k);
+                    if (k + 1u < K) st32a2_nt(Dp + 2u * k, pairs2_at(k));
                     else if (k < K) *reinterpret_cast<uint16_t *>(Dp + 2u * k) = (uint16_t)pair_at(k);
                 } else {
                     for (uint32_t k0 = 0; k0 < K; k0 += 64) {
