@@ -33,8 +33,11 @@
 // (CLOCK_MONOTONIC, shared by both processes) and its mismatch count through a pipe.  One JSON line
 // on stdout.
 #include <dlfcn.h>
+#include <sys/prctl.h>
 #include <sys/wait.h>
 #include <unistd.h>
+
+#include <csignal>
 
 #include <psyne_amd/tdt_substrate.hpp>
 
@@ -120,11 +123,15 @@ int main(int argc, char **argv) {
             return 2;
         }
         std::fflush(nullptr);
+        const pid_t parent = ::getpid();
         child = ::fork();
         if (child < 0) {
             std::perror("fork");
             return 2;
         }
+        // the receiving end never outlives the sending one (a parent that fails must not leave a
+        // child blocked on its socket, and holding the GPU)
+        if (child == 0 && (::prctl(PR_SET_PDEATHSIG, SIGKILL) != 0 || ::getppid() != parent)) std::_Exit(7);
         role = child == 0 ? "rx" : "tx";
         ::close(child == 0 ? rep[0] : rep[1]);
     }
