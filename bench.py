@@ -98,30 +98,54 @@ def free_port() -> int:
     return p
 
 
+# sysfs roots of the topology helpers (tests point them at a fake tree)
+KFD_NODES = "/sys/class/kfd/kfd/topology/nodes"
+SYSFS_DRM = "/sys/class/drm"
+SYSFS_NODE = "/sys/devices/system/node"
+
+
 def visible_gpus() -> list:
     """The GPUs this process may use, found WITHOUT touching HIP (no torch, no HIP runtime: the
     launcher parent must never initialise the GPU): KFD topology nodes with SIMDs
     (/sys/class/kfd/kfd/topology/nodes/*/properties), in node order (the HIP device order),
     narrowed by ROCR_VISIBLE_DEVICES, then HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES.  Each entry
     is that node's properties (drm_render_minor, location_id, ...)."""
-    root = pathlib.Path("/sys/class/kfd/kfd/topology/nodes")
+    root = pathlib.Path(KFD_NODES)
     gpus = []
     try:
-        for d in sorted(root.iterdir(), key=lambda q: int(q.name) if q.name.isdigit() else 1 << 30):
-            props = {}
-            for line in (d / "properties").read_text().splitlines():
-                f = line.split()
-                if len(f) == 2 and f[1].lstrip("-").isdigit():
-                    props[f[0]] = int(f[1])
-            if props.get("simd_count", 0) > 0:
-                gpus.append(props)
-    except (OSError, ValueError):
+        nodes = sorted(root.iterdir(), key=lambda q: int(q.name) if q.name.isdigit() else 1 << 30)
+    except OSError:
         return []
+    for d in nodes:
+        # A node this process may not read is a GPU it cannot open either (the 1-GPU boxes expose
+        # one render node and deny the others' properties): skip it, do not give up on the rest
+        # (round 4's helper returned [] there, so numa_bind never ran on a real box).
+        try:
+            text = (d / "properties").read_text()
+        except OSError:
+            continue
+        props = {}
+        for line in text.splitlines():
+            f = line.split()
+            if len(f) == 2 and f[1].lstrip("-").isdigit():
+                props[f[0]] = int(f[1])
+        if props.get("simd_count", 0) > 0:
+            gpus.append(props)
     for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
         v = os.environ.get(var)
-        if v is not None and v.strip() != "":
-            idx = [int(x) for x in v.split(",") if x.strip().isdigit()]
-            gpus = [gpus[i] for i in idx if 0 <= i < len(gpus)]
+        if v is None or v.strip() == "":
+            continue
+        sel = []
+        for tok in (t.strip() for t in v.split(",")):
+            if tok.isdigit():
+                i = int(tok)
+                if 0 <= i < len(gpus):
+                    sel.append(gpus[i])
+            elif tok.upper().startswith("GPU-"):
+                # UUID form: GPU-<unique_id as 16 hex digits> (rocm-smi / ROCr spelling)
+                want = tok[4:].lower()
+                sel += [g for g in gpus if "unique_id" in g and ("%016x" % g["unique_id"]) == want.rjust(16, "0")]
+        gpus = sel
     return gpus
 
 
@@ -144,13 +168,13 @@ def numa_bind(local_rank: int):
         return None
     minor = gpus[local_rank]["drm_render_minor"]
     try:
-        node = int(pathlib.Path("/sys/class/drm/renderD%d/device/numa_node" % minor).read_text())
+        node = int(pathlib.Path(SYSFS_DRM, "renderD%d" % minor, "device", "numa_node").read_text())
     except (OSError, ValueError):
         return None
     if node < 0:
         return {"numa_node": node, "bound": False}
     try:
-        cpus = parse_cpulist(pathlib.Path("/sys/devices/system/node/node%d/cpulist" % node).read_text())
+        cpus = parse_cpulist(pathlib.Path(SYSFS_NODE, "node%d" % node, "cpulist").read_text())
         allowed = os.sched_getaffinity(0) & cpus
         if not allowed:
             return {"numa_node": node, "bound": False}
@@ -169,8 +193,15 @@ def launch_ranks(a) -> int:
     if not shared:
         have = len(visible_gpus())
         if have < a.gpus:
-            print("bench.py: --gpus %d but only %d visible GPU(s)" % (a.gpus, have), file=sys.stderr, flush=True)
-            return 2
+            # The topology count is advisory up to one node's worth of GPUs (8): sysfs may hide
+            # nodes this process can still use, or be unreadable, so up to 8 ranks start anyway and
+            # each checks its own device count (main(): a rank whose LOCAL_RANK has no device exits
+            # with status 2).  More than a node's worth beyond what the topology shows is refused.
+            if a.gpus > max(have, 8):
+                print("bench.py: --gpus %d but only %d visible GPU(s)" % (a.gpus, have), file=sys.stderr, flush=True)
+                return 2
+            print("bench.py: --gpus %d, the KFD topology shows %d visible GPU(s); starting the ranks, each checks "
+                  "its device" % (a.gpus, have), file=sys.stderr, flush=True)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(a.gpus),
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()), str(ROOT / "bench.py")] + sys.argv[1:]
     env = dict(os.environ)
@@ -534,6 +565,10 @@ def main():
     shared = os.environ.get("PSYNE_BENCH_SHARED_DEVICE") == "1"
     if shared:
         local = 0
+    elif local >= torch.cuda.device_count():
+        print("bench.py: rank %d has LOCAL_RANK %d but sees %d GPU(s)" % (rank, local, torch.cuda.device_count()),
+              file=sys.stderr, flush=True)
+        sys.exit(2)
     if world > 1:
         torch.cuda.set_device(local)
         if shared:

@@ -132,3 +132,56 @@ def test_visible_gpus_and_cpulist_parsing(tmp_path, monkeypatch):
     assert bench.parse_cpulist("0-3,8,10-11\n") == {0, 1, 2, 3, 8, 10, 11}
     monkeypatch.setenv("ROCR_VISIBLE_DEVICES", "-1")
     assert bench.visible_gpus() == []
+
+
+def _fake_sysfs(tmp_path, monkeypatch):
+    """The layout a 1-GPU MI355X box showed (gpurun_out/r05_a/topo.txt): two CPU nodes, seven
+    GPU nodes this process may not read, one readable GPU node (render minor 160, NUMA node 1)."""
+    import bench
+    kfd, drm, node = tmp_path / "kfd", tmp_path / "drm", tmp_path / "node"
+    for i in range(10):
+        d = kfd / str(i)
+        d.mkdir(parents=True)
+        if i in (0, 1):
+            (d / "properties").write_text("cpu_cores_count 128\nsimd_count 0\ndrm_render_minor 0\n")
+        elif i == 6:
+            (d / "properties").write_text("simd_count 1024\ndrm_render_minor 160\nlocation_id 62464\n"
+                                          "unique_id 12784088038668414734\n")
+        # other nodes: no readable properties (the box answered EPERM)
+    (drm / "renderD160" / "device").mkdir(parents=True)
+    (drm / "renderD160" / "device" / "numa_node").write_text("1\n")
+    allowed = sorted(os.sched_getaffinity(0))
+    (node / "node1").mkdir(parents=True)
+    (node / "node1" / "cpulist").write_text("%d-%d\n" % (allowed[0], allowed[-1]))
+    monkeypatch.setattr(bench, "KFD_NODES", str(kfd))
+    monkeypatch.setattr(bench, "SYSFS_DRM", str(drm))
+    monkeypatch.setattr(bench, "SYSFS_NODE", str(node))
+    for v in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(v, raising=False)
+    return bench
+
+
+def test_visible_gpus_skips_unreadable_nodes(tmp_path, monkeypatch):
+    """Round 4's helper gave up on the first unreadable node, so every box run reported numa: null
+    (VERDICT r04 item 3): unreadable nodes are skipped, the readable GPU is found, indices and
+    UUIDs in the visibility variables select it, and numa_bind binds to its node."""
+    bench = _fake_sysfs(tmp_path, monkeypatch)
+    g = bench.visible_gpus()
+    assert [x["drm_render_minor"] for x in g] == [160]
+    monkeypatch.setenv("ROCR_VISIBLE_DEVICES", "0")
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0")
+    assert len(bench.visible_gpus()) == 1
+    monkeypatch.setenv("ROCR_VISIBLE_DEVICES", "GPU-%016x" % 12784088038668414734)
+    assert len(bench.visible_gpus()) == 1
+    monkeypatch.setenv("ROCR_VISIBLE_DEVICES", "GPU-0123456789abcdef")
+    assert bench.visible_gpus() == []
+    monkeypatch.setenv("ROCR_VISIBLE_DEVICES", "1")
+    assert bench.visible_gpus() == []
+    monkeypatch.setenv("ROCR_VISIBLE_DEVICES", "0")
+    before = os.sched_getaffinity(0)
+    try:
+        r = bench.numa_bind(0)
+    finally:
+        os.sched_setaffinity(0, before)
+    assert r == {"numa_node": 1, "bound": True, "cpus": len(before)}
+    assert bench.numa_bind(1) is None
