@@ -131,7 +131,9 @@ struct EncLayout {
     static constexpr int W = TEAM / 64;
     static constexpr int WPG = 16 / WS;  // words per 16-byte group
     // histogram, per byte position (uint32): bins 1..255 x HC copies (bin v copy k at
-    // (v - 1)·HC + k), one unused row, then 64 per-lane zero bins at ZB + lane.
+    // (v - 1)·HC + k), one unused row, then 64 (unused) dwords.  Zero bytes are not counted in
+    // LDS: their atomic is aimed past the allocation (dropped) and the zero count is the words
+    // minus the nonzero total (round 5).
     // 16 KiB of copies whatever the word size for message-sized teams; one copy for the
     // one-wave small-message kernel (its LDS footprint sets how many messages a CU holds)
     static constexpr int HC = TEAM >= 256 ? 16 / WS : 1;
@@ -167,7 +169,7 @@ struct EncLayout {
     static constexpr int REGION = STAGE > ANALYSIS ? STAGE : ANALYSIS;
     static constexpr int SLOTS = W * 8 * 4;
     static constexpr int MISC = 512;
-    static constexpr int WM = 160;  // mapping state (uint32)
+    static constexpr int WM = 176;  // mapping state (uint32)
     static constexpr int OFF_HIST = 0;
     static constexpr int OFF_TERMS = HISTA;
     static constexpr int OFF_LOG2 = HISTA + TERMS;
@@ -185,7 +187,8 @@ enum {
     M_MSG = 0, M_NS = 1, M_L0 = 2, M_K0 = 3, M_K1 = 4, M_SELA = 8 /*4*/, M_SELB = 12 /*4*/, M_EDA = 16,
     M_EDB = 17, M_EXACT = 18, M_STATUS = 26, M_MAP = 32 /*16*/, M_ENT = 64 /*16 doubles*/, M_BASE = 96 /*u64*/,
     M_SB = 100 /*16*/, M_PART = 128 /*16 doubles: per-wave entropy partials*/, M_Z = 48 /*16: zero-bin totals*/,
-    M_MAPBITS = 5 /*bit b = mapping[b]*/, M_READY = 6 /*deferred look-back: offset published*/
+    M_MAPBITS = 5 /*bit b = mapping[b]*/, M_READY = 6 /*deferred look-back: offset published*/,
+    M_CPART = 160 /*16: per-wave (or per-position) nonzero byte counts*/
 };
 // decision margin of the mapping fast path, in bits of entropy: > 2x its worst-case error
 // delta <= 2^-18 (hardware log2 per count) + 5·2^-24·log2 N (float sums of <= 4 bins, plus the
@@ -672,10 +675,11 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
             const uint32_t nsp = (lm->ntiles + kSpanTiles - 1) / kSpanTiles;
             const uint32_t *sh = a.shist + (uint64_t)lm->span0 * WS * 256;
             for (int i = tid; i < WS * 256; i += TEAM) {
+                const int v = i & 255;
+                if (v == 0) continue;  // (the zero count is derived from the nonzero total below)
                 uint32_t c = 0;
                 for (uint32_t k = 0; k < nsp; ++k) c += sh[(uint64_t)k * WS * 256 + i];
-                const int v = i & 255;
-                hist[(i >> 8) * Lay::PS + (v ? Lay::bin(v, 0) : Lay::ZB)] = c;
+                hist[(i >> 8) * Lay::PS + Lay::bin(v, 0)] = c;
             }
         }
         // glibc log2 tables → LDS (the bins' log2 evaluations read them with per-lane indices)
@@ -686,13 +690,14 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
         }
         team_sync<W>();
         // Compare-free bin address: v·4HC + 4(copy - HC) is bin v's copy for v >= 1 and wraps
-        // to >= 2^16 - 4HC for v = 0, so min() with this lane's zero bin (above every bin)
-        // selects it.  Two bytes per instruction in u16 halves (v_perm → v_pk_mad_u16 →
-        // v_pk_min_u16, then v_and / v_lshrrev split the two addresses): 16 cycles per two
-        // bytes instead of three 4-cycle ops per byte.
-        const uint32_t zoff = (uint32_t)(Lay::ZB + lane) * 4u;
+        // to >= 2^16 - 4HC for v = 0: an address past every encode workgroup's LDS allocation,
+        // so the zero byte's atomic is dropped (tools/ubench_lds.hip: out-of-range ds_add lands
+        // nowhere) and the zero count is derived from the nonzero total.  Two bytes per
+        // instruction in u16 halves (v_pk_mad_u16, then v_and / v_lshrrev split the two
+        // addresses): round 4's per-lane zero bins took a v_pk_min_u16 per byte pair more.
+        static_assert(Lay::BYTES <= 65536 - 4 * Lay::HC, "zero-byte atomics must fall past the allocation");
         const uint32_t coff = (((uint32_t)lane & (Lay::HC - 1)) - (uint32_t)Lay::HC) * 4u;
-        const uint32_t coff2 = (coff & 0xffffu) * 0x10001u, zoff2 = zoff * 0x10001u;
+        const uint32_t coff2 = (coff & 0xffffu) * 0x10001u;
         constexpr uint32_t kMul2 = (uint32_t)(4 * Lay::HC) * 0x10001u;
         auto hist_group = [&](const uint4 &d, uint32_t vb, bool full) __attribute__((always_inline)) {
             const uint32_t dw[4] = {d.x, d.y, d.z, d.w};
@@ -704,7 +709,6 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
                 const uint32_t P = (o ? dw[w] >> 8 : dw[w]) & 0x00ff00ffu;
                 uint32_t A;
                 asm("v_pk_mad_u16 %0, %1, %2, %3" : "=v"(A) : "v"(P), "s"(kMul2), "v"(coff2));
-                asm("v_pk_min_u16 %0, %1, %2" : "=v"(A) : "v"(A), "v"(zoff2));
                 const uint32_t ad2[2] = {A & 0xffffu, A >> 16};
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
@@ -750,16 +754,25 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
             }
         }
         if constexpr (TL == 1) {
-            // the span's histogram (its LDS copies and zero bins summed), for the map pass
+            // the span's histogram (its LDS copies summed; the zero count = the span's words
+            // minus its nonzero total), for the map pass
             uint32_t *sh = a.shist + ((uint64_t)a.lmeta[lj].span0 + tile) * WS * 256;
+            uint32_t *tot = wm + M_CPART;
+            if (tid < WS) tot[tid] = 0u;
+            team_sync<W>();
             for (int i = tid; i < WS * 256; i += TEAM) {
                 const int b = i >> 8, v = i & 255;
+                if (v == 0) continue;
                 uint32_t c = 0;
 #pragma unroll
-                for (int k = 0; k < Lay::HC; ++k) c += v ? hist[b * Lay::PS + Lay::bin(v, k)] : 0u;
-                if (v == 0)
-                    for (int z = 0; z < 64; ++z) c += hist[b * Lay::PS + Lay::ZB + z];
+                for (int k = 0; k < Lay::HC; ++k) c += hist[b * Lay::PS + Lay::bin(v, k)];
                 sh[i] = c;
+                if (c) atomicAdd(&tot[b], c);
+            }
+            team_sync<W>();
+            if (tid < WS) {
+                const uint64_t t0 = 16ull * kTG * tile, sb = n - t0 < 16ull * kTG ? n - t0 : 16ull * kTG;
+                sh[tid * 256] = (uint32_t)(sb / WS) - tot[tid];
             }
             return;
         }
@@ -782,7 +795,7 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
         // :507-525).  Otherwise — ties: constant or repeated-distribution data — the exact fma chains in
         // bin order decide (below).  The sweep costs one log per bin and one reduction per position.
         uint32_t exact_needed = 1;
-        if constexpr (MODE != MODE_ANALYZE) {
+        {
             constexpr int TP = TEAM / WS;  // threads per position (4 .. 512)
             constexpr int BPT = TP >= 256 ? 1 : 256 / TP;
             const int pb = tid / TP, pj = tid % TP;
@@ -792,6 +805,7 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
             // fmas of a group) add at most 5·2^-24·log2 N < 9.6e-6 bits to the hardware log's
             // 2^-18
             double acc = 0.0;
+            uint32_t ci = 0;  // nonzero bytes of the position counted by this thread's bins
 #pragma unroll
             for (int k0 = 0; k0 < BPT; k0 += kFloatGroup) {
                 float accf = 0.0f;
@@ -799,42 +813,53 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
                 for (int k = k0; k < (k0 + kFloatGroup < BPT ? k0 + kFloatGroup : BPT); ++k) {
                     const int v = pj + k * TP;
                     if (TP > 256 && v >= 256) break;  // (TEAM 512, word size 1: half the team idle)
-                    const float cf = (float)count(pb, v);  // (0 for v = 0: the zero bins are summed below)
-                    accf = __builtin_fmaf(cf, __builtin_amdgcn_logf(__builtin_fmaxf(cf, 1.0f)), accf);
+                    const uint32_t c = count(pb, v);  // (0 for v = 0: its count is derived below)
+                    ci += c;
+                    if constexpr (MODE != MODE_ANALYZE) {
+                        const float cf = (float)c;
+                        accf = __builtin_fmaf(cf, __builtin_amdgcn_logf(__builtin_fmaxf(cf, 1.0f)), accf);
+                    }
                 }
                 acc += (double)accf;
             }
+            uint32_t *cpart = wm + M_CPART;
             if constexpr (TP >= 64) {
-                acc = seg_sum_f64<64>(acc);
-                if (lane == 63) part[wv] = acc;  // wave wv: TP / 64 waves per position
+                if constexpr (MODE != MODE_ANALYZE) acc = seg_sum_f64<64>(acc);
+                ci = seg_sum_u32<64>(ci);
+                if (lane == 63) {  // wave wv: TP / 64 waves per position
+                    part[wv] = acc;
+                    cpart[wv] = ci;
+                }
             } else {
-                acc = seg_sum_f64<TP>(acc);
-                if (pj == TP - 1) part[pb] = acc;
-            }
-            // zero bins (wave 0): LPP lanes per position, WS zero bins per lane
-            if (wv == 0) {
-                constexpr int LPP = 64 / WS;
-                const int zb = lane / LPP, zl = lane % LPP;
-                uint32_t z = 0;
-#pragma unroll
-                for (int q = 0; q < WS; ++q) z += hist[zb * Lay::PS + Lay::ZB + zl + q * LPP];
-                z = seg_sum_u32<LPP>(z);
-                if (zl == LPP - 1) wm[M_Z + zb] = z;
+                if constexpr (MODE != MODE_ANALYZE) acc = seg_sum_f64<TP>(acc);
+                ci = seg_sum_u32<TP>(ci);
+                if (pj == TP - 1) {
+                    part[pb] = acc;
+                    cpart[pb] = ci;
+                }
             }
             team_sync<W>();
             if (wv == 0) {
+                // zero count of position lane: its words minus its nonzero bytes
+                uint32_t nz = 0;
                 double sb = 0.0;
                 if (lane < WS) {
                     if constexpr (TP >= 64) {
 #pragma unroll
                         for (int w = 0; w < W; ++w)
-                            if (w * 64 / TP == lane) sb += part[w];
+                            if (w * 64 / TP == lane) {
+                                sb += part[w];
+                                nz += cpart[w];
+                            }
                     } else {
                         sb = part[lane];
+                        nz = cpart[lane];
                     }
-                    const uint32_t z = wm[M_Z + lane];
+                    const uint32_t z = wc - nz;
+                    wm[M_Z + lane] = z;
                     if (z) sb += (double)z * (double)__builtin_amdgcn_logf((float)z);
                 }
+              if constexpr (MODE != MODE_ANALYZE) {
                 double ss = 0.0;
 #pragma unroll
                 for (int b = 0; b < WS; ++b) ss += readlane_f64(sb, b);
@@ -847,9 +872,10 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
                     wm[M_EXACT] = fast ? 0u : 1u;
                     if (fast) wm[M_MAPBITS] = mbits;
                 }
+              }
             }
             team_sync<W>();
-            exact_needed = __builtin_amdgcn_readfirstlane(wm[M_EXACT]);
+            if constexpr (MODE != MODE_ANALYZE) exact_needed = __builtin_amdgcn_readfirstlane(wm[M_EXACT]);
         }
 #ifdef PSY_X_FIXMAP
         exact_needed = 0;  // diagnostic: no entropy terms / chains
@@ -935,10 +961,7 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
                     double np = 0.0, L = 0.0;
                     if (b < WS) {
                         uint32_t c = count(b, i & 255);
-                        if ((i & 255) < 64) {  // wave-uniform: bin 0 adds the 64 per-lane zero bins
-                            const uint32_t z = wave_reduce<OpAdd>(hist[b * Lay::PS + Lay::ZB + lane]);
-                            if (lane == 0) c += z;
-                        }
+                        if ((i & 255) == 0) c = wm[M_Z + b];  // bin 0: the derived zero count
                         if constexpr (MODE == MODE_ANALYZE) {
                             if (a.hist_out) a.hist_out[((uint64_t)msg * WS + b) * 256 + (i & 255)] = c;
                         }
