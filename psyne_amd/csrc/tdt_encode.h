@@ -505,12 +505,18 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
     if constexpr (RES) {
         // One unconditional dwordx4 per lane and round, all in flight before the first use (a
         // branchy load per round made the compiler wait for each before issuing the next).
-        // Lanes past the end load the message's first group instead; every pass masks them by
-        // vbytes / vmask.
+        // Raw buffer loads over the message (num_records = n): the round offsets are scalar
+        // and lanes past the end read zeros from the hardware range check, so no per-round
+        // address arithmetic (round 4: a compare, a select and a 64-bit address per round);
+        // every pass masks those lanes by vbytes / vmask.
+        const __amdgpu_buffer_rsrc_t rsrc =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(base), (short)0, (int)n32, 0x00020000);
+        const int vo = (int)((gw0 + (uint32_t)lane) * 16u);
 #pragma unroll
         for (int r = 0; r < G; ++r) {
-            const uint32_t g = gw0 + r * 64 + lane;
-            dres[r] = *reinterpret_cast<const uint4 *>(base + 16ull * (g < ngroups ? g : 0u));
+            typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+            const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, vo, r * 1024, 0);
+            dres[r] = make_uint4(v.x, v.y, v.z, v.w);
             cres[r] = 0;
         }
     }
