@@ -308,6 +308,19 @@ __device__ __forceinline__ uint32_t rdlane(uint32_t x, int l) {
 __device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel) {
     return __builtin_amdgcn_perm(hi, lo, sel);
 }
+// Byte-lane layout of a group's 16 slot bits (resident bodies, word size <= 4): slot j = 4t + q
+// at bit 8t + q, the position the SWAR zero-byte test of T[q] leaves it in, so that pass A1
+// skips the compaction into 16 bits (round 5).  Monotonic in j, so hibit / lobit / "a bit above
+// a low mask" keep their meaning; sb_slot maps a bit position back to the slot.
+__host__ __device__ constexpr uint32_t sb_pos(uint32_t j) { return 8u * (j >> 2) + (j & 3u); }
+__host__ __device__ constexpr uint32_t sb_slot(uint32_t b) { return ((b >> 3) << 2) | (b & 3u); }
+__device__ __forceinline__ uint32_t sb_spread(uint32_t x) {  // 16-bit compact -> byte-lane
+    return (x & 0xfu) | ((x & 0xf0u) << 4) | ((x & 0xf00u) << 8) | ((x & 0xf000u) << 12);
+}
+__device__ __forceinline__ uint32_t sb_compact(uint32_t x) {  // byte-lane -> 16-bit compact
+    x = (x | (x >> 4)) & 0x00ff00ffu;
+    return (x | (x >> 8)) & 0xffffu;
+}
 // bit j of e duplicated into bits 2j and 2j+1 (16 → 32 bits)
 __device__ __forceinline__ uint32_t spread2(uint32_t e) {
     uint32_t x = e & 0xffffu;
@@ -474,9 +487,12 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
         if (vb == 0) return make_uint4(0, 0, 0, 0);
         return ld16_any(base + 16ull * g, (int)vb);
     };
-    // FULL round: its 64 groups all hold 16 message bytes (uniform)
+    // FULL round: its 64 groups all hold 16 message bytes (uniform; 32-bit so that it stays
+    // on the scalar unit: gfx9 has no 64-bit scalar ordered compare, and the u64 form cost a
+    // VGPR copy, two v_cmp_*_u64 and a select per round)
+    const uint32_t nfull = n32 >> 4;  // whole groups of the message
     auto full_round = [&](uint32_t r) __attribute__((always_inline)) -> bool {
-        return 16ull * (gw0 + r * 64 + 64) <= n;
+        return gw0 + r * 64u + 64u <= nfull;
     };
 
     // The rest of the kernel is instantiated twice: RES (the message's RW <= G rounds stay in
@@ -529,7 +545,7 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
         } else {
             // rounds r < RW of the wave that hold a group of the message (uniform)
             auto live = [&](uint32_t r) __attribute__((always_inline)) {
-                return r < RW && 16ull * (gw0 + r * 64) < n;
+                return r < RW && gw0 + r * 64u < ngroups;
             };
             if constexpr (PF == 1) {
                 for (uint32_t r = 0; live(r); ++r) {
@@ -1145,6 +1161,13 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
         const bool ns2 = ns == 2;
         const uint32_t Ls[2] = {L0, ns2 ? 16u - L0 : 0u};
         const uint32_t lowL0 = L0 >= 16 ? 0xffffu : ((1u << L0) - 1u);
+        // start masks of the resident word-size <= 4 bodies are kept in the byte-lane layout
+        // (sb_pos); everything else (streaming bodies, tiles' count pass, A2's scans) in the
+        // compact 16-bit one
+        constexpr bool BL = RES && WS <= 4 && TL != 2;
+        const uint32_t lowX = BL ? sb_spread(lowL0) : lowL0;   // stream-0 slots
+        const uint32_t highX = BL ? sb_spread(~lowL0 & 0xffffu) : (~lowL0 & 0xffffu);  // stream-1 slots
+        const uint32_t fullX = BL ? 0x0f0f0f0fu : 0xffffu;
         // selectors extracting slot L0 (stream 1's first byte) from T: slot j is byte j/4 of
         // T[j%4], i.e. byte (j%4 & 1)*4 + j/4 of perm(T[1],T[0]) or perm(T[3],T[2])
         uint32_t fsA = 0x0c0c0c0cu, fsB = 0x0c0c0c0cu;
@@ -1178,8 +1201,10 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
         constexpr bool kFold = WS <= 4;  // L0 = (16 / WS)·k0 is then a multiple of 4
         const uint32_t p0sel = kFold && ns2 ? (0x06050400u & ~(0xffu << (2u * L0))) | (0x01u << (2u * L0)) : 0x06050400u;
         // first: this round holds the message's group 0 (uniform)
-        auto run_mask = [&](const uint32_t (&T)[4], uint32_t ed, uint32_t edc, bool first,
-                            uint32_t V) __attribute__((always_inline)) -> uint32_t {
+        // (BLM: the byte-lane layout, V given in it too)
+        auto run_mask = [&](const uint32_t (&T)[4], uint32_t ed, uint32_t edc, bool first, uint32_t V,
+                            auto blm) __attribute__((always_inline)) -> uint32_t {
+            constexpr bool BLM = decltype(blm)::value;
             const uint32_t pe = wave_shr1(ed, edc);  // previous group's edges
             const uint32_t P0 = perm(T[3], pe, p0sel);
             const uint32_t X[4] = {T[0] ^ P0, T[1] ^ T[0], T[2] ^ T[1], T[3] ^ T[2]};
@@ -1188,6 +1213,10 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
             for (int q = 0; q < 4; ++q) {
                 const uint32_t y = ((X[q] & 0x7f7f7f7fu) + 0x7f7f7f7fu) | X[q];
                 m |= (y >> (7 - q)) & (0x01010101u << q);
+            }
+            if constexpr (BLM) {
+                if (first && lane == 0) m |= 1u | (ns2 ? (1u << sb_pos(L0)) : 0u);
+                return m & V;
             }
             m = (m | (m >> 4)) & 0x00ff00ffu;
             m = (m | (m >> 8)) & 0xffffu;
@@ -1304,13 +1333,13 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
                 const uint32_t ed = edges(d);
                 uint32_t T[4];
                 tmat(d, T);
-                const uint32_t V = full_round(r) ? 0xffffu : vmask(vbytes(g));
-                const uint32_t m = run_mask(T, ed, edc, r == 0u && gw0 == 0u, V);
+                const uint32_t V = full_round(r) ? fullX : (BL ? sb_spread(vmask(vbytes(g))) : vmask(vbytes(g)));
+                const uint32_t m = run_mask(T, ed, edc, r == 0u && gw0 == 0u, V, std::integral_constant<bool, BL>{});
                 edc = rdlane(ed, 63);
                 cm = m;
                 if constexpr (decltype(res)::value) d = make_uint4(T[0], T[1], T[2], T[3]);
                 constexpr bool SW = decltype(res)::value && TL != 2;  // scalar last-start tracking
-                const uint32_t m0 = m & lowL0;
+                const uint32_t m0 = m & lowX;
                 const uint64_t r0 = (uint64_t)__ballot(m0 != 0u);
                 if constexpr (SW) {
                     if (r0) {
@@ -1328,8 +1357,8 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
                 const uint64_t b0 = r0 | pastm;
                 zacc |= (b0 - zk1[0]) & ~b0 & zk8[0];
                 if (ns2) {
-                    const uint32_t m1 = m >> L0;
-                    const uint64_t r1 = (uint64_t)__ballot(m > lowL0);  // m1 != 0 (m < 2^16)
+                    const uint32_t m1 = BL ? m & highX : m >> L0;
+                    const uint64_t r1 = (uint64_t)__ballot(m > lowX);  // m1 != 0 (layouts monotonic in the slot)
                     if constexpr (SW) {
                         if (r1) {
                             lr[1] = r;
@@ -1358,8 +1387,10 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
 #pragma unroll
                 for (int r = 0; r < GR; ++r)
                     if ((uint32_t)r == lr[c]) mv = rdlane(cres[r], (int)l);
-                const uint32_t mc = c ? mv >> L0 : mv & lowL0;
-                wmax[c] = (gw0 + lr[c] * 64u + l) * Ls[c] + hibit(mc) + 1u;
+                uint32_t hb;
+                if constexpr (BL) hb = sb_slot(hibit(c ? mv & highX : mv & lowX)) - (c ? L0 : 0u);
+                else hb = hibit(c ? mv >> L0 : mv & lowL0);
+                wmax[c] = (gw0 + lr[c] * 64u + l) * Ls[c] + hb + 1u;
             }
         } else {
             wmax[0] = wave_reduce<OpMax>(wmax[0]);
@@ -1419,16 +1450,16 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
                 const uint32_t V = full_round(r) ? 0xffffu : vmask(vbytes(g));
                 uint32_t m;
                 if constexpr (decltype(res)::value) {
-                    m = cm;
+                    m = BL ? sb_compact(cm) : cm;
                 } else {
                     uint32_t T[4];
                     tmat(d, T);
                     const uint32_t ed = edges(d);
-                    m = run_mask(T, ed, edc, r == 0u && gw0 == 0u, V);
+                    m = run_mask(T, ed, edc, r == 0u && gw0 == 0u, V, std::false_type{});
                     edc = rdlane(ed, 63);
                 }
                 const uint32_t C = chunk_round(r, m, rcarry, g, V);
-                cm = C;
+                cm = BL ? sb_spread(C) : C;
                 pc0 += popc(C & lowL0);
                 pc1 += popc(C >> L0);
             });
@@ -1707,11 +1738,12 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
                 pos6[q] = ((x & 0x7f7f7f7fu) + jq) ^ (x & 0x80808080u);
             }
         }
+        // C in the byte-lane layout for the resident body (BL), compact for the streaming one
         auto sweep6 = [&](const uint4 &Tw, uint32_t C) __attribute__((always_inline)) {
             PSY_ASM_ROUND(B);
             const uint32_t T[4] = {Tw.x, Tw.y, Tw.z, Tw.w};
-            const uint32_t c0 = popc(C & lowL0);
-            const uint32_t pc = c0 | (popc(C >> L0) << 16);
+            const uint32_t c0 = popc(C & lowX);
+            const uint32_t pc = c0 | (popc(C & highX) << 16);
             const uint32_t pinc = wave_incl_scan<OpAdd>(pc);
             const uint32_t pexc = pinc - pc;
             const uint32_t Stot = rdlane(pinc, 63);
@@ -1731,7 +1763,7 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
             for (int j = 0; j < 16; ++j) {
                 const int q = j & 3, t = j >> 2;
                 if (j > 0 && j % WPG == 0 && (uint32_t)j == L0) D = D1;  // stream 1 begins (uniform)
-                const uint32_t bit = (C >> j) & 1u;
+                const uint32_t bit = (C >> (BL ? sb_pos(j) : j)) & 1u;
                 uint32_t ad;
                 asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(ad) : "v"(bit), "v"(D), "v"(jl));
                 const uint32_t e = E[q][t >> 1];
@@ -1921,7 +1953,7 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
                 tmat(d, T);
                 Tw = make_uint4(T[0], T[1], T[2], T[3]);
                 const uint32_t ed = edges(d);
-                const uint32_t m = run_mask(T, ed, edc, r == 0u && gw0 == 0u, V);
+                const uint32_t m = run_mask(T, ed, edc, r == 0u && gw0 == 0u, V, std::false_type{});
                 edc = rdlane(ed, 63);
                 return clean ? m : chunk_round(r, m, rcarry, g, V);
             };
