@@ -1803,20 +1803,29 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
                     return perm(E01, d, 0x07020500u);
                 };
                 if (((uintptr_t)Dp & 1) == 0) {
-                    // lane l stores pairs k0 + 2l, k0 + 2l + 1 with one (2-byte aligned) dword store
+                    // lane l stores pairs k0 + 2l, k0 + 2l + 1 with one (2-byte aligned) dword store.
+                    // Non-temporal stores only where a store instruction's 256 bytes cannot hold
+                    // the flush's first or last (partial) 128-byte line: plain stores leave those
+                    // in L2, where the neighbouring flush's half of the line merges with them
+                    // (round 4 wrote every pair non-temporally: 15.86 GB per C3 launch for 13.74 GB
+                    // of blobs).  The choice is uniform per store instruction.
+                    auto st_pair2 = [&](uint32_t k, uint32_t v, bool edge) __attribute__((always_inline)) {
+                        if (edge) *reinterpret_cast<u32_a2 *>(Dp + 2u * k) = v;
+                        else st32a2_nt(Dp + 2u * k, v);
+                    };
                     uint32_t k0 = 0;
                     for (; k0 + 256u <= K; k0 += 256u) {
                         const uint32_t k = k0 + 2u * (uint32_t)lane;
                         const uint32_t pa = pairs2_at(k), pb = pairs2_at(k + 128u);
-                        st32a2_nt(Dp + 2u * k, pa);
-                        st32a2_nt(Dp + 2u * k + 256u, pb);
+                        st_pair2(k, pa, k0 == 0u);
+                        st_pair2(k + 128u, pb, K - k0 < 256u + 64u);
                     }
                     for (; k0 + 128u <= K; k0 += 128u) {
                         const uint32_t k = k0 + 2u * (uint32_t)lane;
-                        st32a2_nt(Dp + 2u * k, pairs2_at(k));
+                        st_pair2(k, pairs2_at(k), k0 == 0u || K - k0 < 128u + 64u);
                     }
                     const uint32_t k = k0 + 2u * (uint32_t)lane;
-                    if (k + 1u < K) st32a2_nt(Dp + 2u * k, pairs2_at(k));
+                    if (k + 1u < K) *reinterpret_cast<u32_a2 *>(Dp + 2u * k) = pairs2_at(k);
                     else if (k < K) *reinterpret_cast<uint16_t *>(Dp + 2u * k) = (uint16_t)pair_at(k);
                 } else {
                     for (uint32_t k0 = 0; k0 < K; k0 += 64) {
