@@ -318,8 +318,9 @@ def cpu_baseline(data_u8, msg_bytes, target_s, threads, kind):
     """CPU rows of the REFERENCE codec (oracle/_ref, the reference header compiled where it lies)
     on bounded samples of the same messages, sample_fraction 0.3 (reference default) and 1.0
     (parity mode), one protocol object per thread: 1 thread, and `threads` workers pinned one per
-    physical core (default: every physical core of the host); plus a 16-thread
-    row (the one-GPU box's CPU share).  The multi-thread rows run over 4 GiB of DISTINCT messages
+    physical core (default: every physical core of the host); plus 16-, 32- and
+    64-thread rows (16 = the one-GPU box's CPU share).  `value` is the best sample-0.3 row and
+    `cores` its thread count.  The multi-thread rows run over 4 GiB of DISTINCT messages
     (no cache-resident working set), repeated to last about 2 s; the 1-thread rows over as many
     distinct messages as take about `target_s`."""
     import numpy as np
@@ -344,7 +345,10 @@ def cpu_baseline(data_u8, msg_bytes, target_s, threads, kind):
         for sf in (0.3, 1.0):
             t1, _ = ref.bench(sample[: 16 * msg_bytes], off[:17], sample_fraction=sf, threads=1, reps=1)
             per_msg = t1 / 16
-            for thr in ((1, 16, threads) if sf == 0.3 else (1, threads)):
+            # (sample 0.3: 1 thread, 16 (the one-GPU box's CPU share), 32, 64 and every physical
+            # core — the reference stops scaling well before all cores, so the best row is reported)
+            thr_list = sorted({1, 16, 32, 64, threads} if sf == 0.3 else {1, threads})
+            for thr in (t for t in thr_list if t <= max(threads, 1) or t == 1):
                 if thr > 1:
                     k, reps = n_big, 1  # (one pass over 4 GiB: 2.5-3 s on the MI355X box's host)
                     cp = pins if thr == threads else ([cores[i % len(cores)] for i in range(thr)] if pins else None)
@@ -357,12 +361,15 @@ def cpu_baseline(data_u8, msg_bytes, target_s, threads, kind):
                 rows.append(dict(value=payload / secs / 2**30, unit="GiB/s", cores=thr, sample_fraction=sf,
                                  seconds=round(secs, 2), msgs=k, reps=reps, distinct_bytes=k * msg_bytes,
                                  pinned=cp is not None, ratio=float(payload / enc)))
-        main = next(r for r in rows if r["sample_fraction"] == 0.3 and r["cores"] == threads)
-        return dict(value=main["value"], unit="GiB/s", cores=threads, kind="reference",
+        # the baseline is the BEST reference configuration measured (default sample 0.3), with its
+        # thread count (round 4 reported the all-core row, slower than 16 threads)
+        main = max((r for r in rows if r["sample_fraction"] == 0.3), key=lambda r: r["value"])
+        return dict(value=main["value"], unit="GiB/s", cores=main["cores"], kind="reference",
                     sample="%d x %d B distinct msgs (first %.1f GiB of the payload) x %d passes; reference "
                            "encode+decode, sample_fraction 0.3, one object per thread, %d threads pinned one per "
-                           "physical core, %.1f s" % (main["msgs"], msg_bytes, main["distinct_bytes"] / 2**30,
-                                                     main["reps"], threads, main["seconds"]),
+                           "physical core (the best of the rows: 1 / 16 / 32 / 64 / all %d physical cores), %.1f s"
+                           % (main["msgs"], msg_bytes, main["distinct_bytes"] / 2**30, main["reps"], main["cores"],
+                              threads, main["seconds"]),
                     rows=rows, nproc=nproc, lscpu_physical_cores=phys, affinity_cpus=aff_n, affinity_mask=aff)
     orc = Oracle()
     t0 = time.perf_counter()
