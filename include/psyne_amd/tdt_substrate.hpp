@@ -23,8 +23,9 @@
 //     Base: the vtable to implement — psyne::behaviors::SubstrateBehavior in a psyne build
 //     (every method here matches its signature, so it overrides), an empty struct otherwise.
 //     send_batch / receive_batch move many messages per GPU call through the C ABI host
-//     pipeline (tdt_encode_host_v / tdt_decode_host: chunked, H2D / kernel / D2H overlapped on
-//     two streams) with a sender and a receiver thread overlapping the socket with the codec,
+//     pipeline (tdt_encode_host_v / tdt_decode_host: chunked, H2D / kernel / D2H of neighbouring
+//     chunks overlapped over four pipeline slots) with a sender and a receiver thread overlapping
+//     the socket with the codec,
 //     which is how the codec reaches the link's rate instead of per-message latency.
 #pragma once
 
@@ -141,6 +142,19 @@ public:
         if (!read_all(buffer, hdr)) fail("TCP receive failed: connection lost");
         bytes_received_ += hdr + sizeof(hdr);
         packets_received_++;
+    }
+
+    // The length word of the next frame, if it has arrived (nothing is consumed): lets a reader
+    // size its buffer before try_transport_receive, which drops the connection on a frame
+    // larger than the buffer it is given.
+    bool peek_frame_length(size_t &len) {
+        if (!is_connected()) return false;
+        std::lock_guard<std::mutex> lk(rmu_);
+        uint32_t hdr = 0;
+        const ssize_t got = ::recv(fd_, &hdr, sizeof(hdr), MSG_PEEK | MSG_DONTWAIT);
+        if (got < (ssize_t)sizeof(hdr)) return false;
+        len = hdr;
+        return true;
     }
 
     // (:153-194) non-blocking probe: a frame is read only when its length word has arrived;
@@ -338,8 +352,13 @@ public:
         name_ = std::string("TDT+") + inner_.substrate_name();
     }
     ~TdtSubstrate() {
+        // queued frames get a bounded wait to leave (a peer that stopped reading would otherwise
+        // block the destructor for ever); then Inner is closed, which ends a send stuck inside it
         try {
-            if (tx_thread_.joinable()) flush();
+            if (tx_thread_.joinable()) {
+                std::unique_lock<std::mutex> lk(tx_mu_);
+                tx_cv_.wait_for(lk, std::chrono::seconds(5), [&] { return tx_queue_.empty() && !tx_busy_; });
+            }
         } catch (...) {
         }
         {
@@ -353,7 +372,8 @@ public:
         }
         rx_cv_.notify_all();
         if constexpr (requires(Inner &s) { s.close(); }) {
-            if (rx_thread_.joinable()) inner_.close();  // (the receiver may sit inside a read)
+            // (the receiver may sit inside a read, the sender inside a write)
+            if (rx_thread_.joinable() || tx_thread_.joinable()) inner_.close();
         }
         if (tx_thread_.joinable()) tx_thread_.join();
         if (rx_thread_.joinable()) rx_thread_.join();
@@ -387,7 +407,7 @@ public:
         auto pause = std::chrono::microseconds(1);
         while (!try_transport_receive(buffer, buffer_size, got)) {
             if constexpr (requires(Inner &s) { s.is_connected(); }) {
-                if (!inner_.is_connected() && !frames_ready()) throw std::runtime_error("TCP: Not connected");
+                if (!inner_.is_connected() && !frames_pending()) throw std::runtime_error("TCP: Not connected");
             }
             std::this_thread::sleep_for(pause);
             if (pause < std::chrono::microseconds(200)) pause *= 2;
@@ -401,19 +421,38 @@ public:
         if (rx_thread_.joinable()) {
             release_views();
             std::unique_lock<std::mutex> lk(rx_mu_);
-            if (rx_err_ && !rx_front_decoded()) std::rethrow_exception(rx_err_);
+            // (an error is reported once every frame that arrived before it is delivered)
+            if (rx_err_ && rx_drained()) std::rethrow_exception(rx_err_);
             RxBuf *b = rx_front_decoded();
             if (!b) return false;
             const size_t k = b->used;
             rx_consume(1);  // (the frame's payload stays put until its buffer is refilled: see rx_consume)
             const int64_t claimed = b->claim[k];
-            const int32_t st = b->st[k];
-            const uint64_t n = b->doff[k + 1] - b->doff[k];
+            int32_t st = b->st[k];
+            uint64_t n = b->doff[k + 1] - b->doff[k];
             if (claimed > (int64_t)buffer_size) {
                 rx_release_if_done(b);
                 lk.unlock();
                 rx_cv_.notify_all();
                 throw std::runtime_error("TDT: decoded message larger than the buffer");
+            }
+            if (claimed > (int64_t)b->lim) {
+                // over the decoder's limit (the largest max_msg of a receive_batch call) but
+                // within this caller's buffer: decoded now, as receive_batch does
+                const uint64_t fo[2] = {b->off[k], b->off[k + 1]};
+                uint64_t oo[2] = {0, 0};
+                st = TDT_OK;
+                const int rc = tdt_decode_host(codec_.context(), b->mem.data(), fo, 1, static_cast<uint8_t *>(buffer),
+                                               (uint64_t)buffer_size, oo, &st);
+                n = oo[1];
+                rx_release_if_done(b);
+                lk.unlock();
+                rx_cv_.notify_all();
+                if (rc != TDT_OK) throw std::runtime_error(std::string("TDT: GPU decode failed: ") + tdt_last_error());
+                if (st != TDT_OK) throw std::runtime_error(tdt_status_string(st));
+                received_size = n;
+                last_received_ = n;
+                return true;
             }
             if (st == TDT_OK && n) std::memcpy(buffer, b->dec.data() + b->doff[k], n);
             rx_release_if_done(b);
@@ -695,6 +734,7 @@ private:
     static constexpr size_t kRxFrames = 16384;
     static constexpr size_t kRxMax = 16;  // receive buffers at most (32 MiB of frames each)
     static constexpr uint64_t kRxEager = 4ull << 20;  // an idle decoder gets a buffer once it holds this much
+    static constexpr size_t kMaxFrame = 100ull * 1024 * 1024 + 64;  // the reference's frame cap (tcp_simple.hpp:127-134)
 
     using Clock = std::chrono::steady_clock;
     static double since(Clock::time_point t) { return std::chrono::duration<double>(Clock::now() - t).count(); }
@@ -805,6 +845,12 @@ private:
         std::lock_guard<std::mutex> lk(rx_mu_);
         return rx_front_decoded() != nullptr;
     }
+    // frames that arrived and are not yet delivered, decoded or not
+    bool frames_pending() {
+        if (!rx_thread_.joinable()) return false;
+        std::lock_guard<std::mutex> lk(rx_mu_);
+        return !rx_drained();
+    }
     // k frames of the front buffer consumed (rx_mu_ held)
     void rx_consume(size_t k) { rx_order_.front()->used += k; }
     // a fully consumed buffer returns to the ring (rx_mu_ held)
@@ -911,16 +957,41 @@ private:
                 rx_order_.push_back(b);
                 fcap = rx_frame_cap_;
             }
-            b->mem.reserve(std::max<uint64_t>(kRxBytes + fcap, 2 * fcap));
             auto pause = std::chrono::microseconds(1);
             auto last = std::chrono::steady_clock::now();
             const auto tf = Clock::now();
             double slept = 0;
+            try {
+                b->mem.reserve(std::max<uint64_t>(kRxBytes + fcap, 2 * fcap));
+            } catch (...) {
+                rx_fail(b);
+                return;
+            }
             for (;;) {
                 size_t flen = 0;
                 bool got = false;
-                if (b->mem.capacity() - b->off[b->n] >= fcap)
-                    got = inner_.try_transport_receive(b->mem.data() + b->off[b->n], fcap, flen);
+                try {
+                    // a frame larger than the current capacity (a later call's larger messages)
+                    // grows the buffers instead of reaching Inner with too small a buffer, which
+                    // drops the connection; frames above the reference's 100 MB cap
+                    // are left to Inner, which refuses them as the reference does
+                    if constexpr (requires(Inner &s, size_t &l) { s.peek_frame_length(l); }) {
+                        size_t l = 0;
+                        if (inner_.peek_frame_length(l) && l > fcap && l <= kMaxFrame) {
+                            {
+                                std::lock_guard<std::mutex> lk(rx_mu_);
+                                rx_frame_cap_ = std::max<size_t>(rx_frame_cap_, l);
+                            }
+                            fcap = l;
+                            if (b->n == 0) b->mem.reserve(std::max<uint64_t>(kRxBytes + fcap, 2 * fcap));
+                        }
+                    }
+                    if (b->mem.capacity() - b->off[b->n] >= fcap)
+                        got = inner_.try_transport_receive(b->mem.data() + b->off[b->n], fcap, flen);
+                } catch (...) {
+                    rx_fail(b);
+                    return;
+                }
                 if (got) {
                     b->off.push_back(b->off[b->n] + flen);
                     ++b->n;
@@ -973,6 +1044,21 @@ private:
             rx_cv_.notify_all();
         }
     }
+    // the receiver's own failure (allocation, a throwing Inner): recorded for the consumers, what
+    // arrived before it still delivered
+    void rx_fail(RxBuf *b) {
+        {
+            std::lock_guard<std::mutex> lk(rx_mu_);
+            if (!rx_err_) rx_err_ = std::current_exception();
+            if (b->n > 0) {
+                b->sealed = true;
+            } else {
+                rx_order_.pop_back();
+                b->free = true;
+            }
+        }
+        rx_cv_.notify_all();
+    }
     // decoder thread: each sealed buffer's frames on the GPU, in arrival order
     void dec_loop() {
         for (;;) {
@@ -995,16 +1081,16 @@ private:
                 lim = rx_max_msg_;
             }
             const auto td = Clock::now();
-            b->claim.resize(b->n);
-            b->st.assign(b->n, TDT_OK);
-            b->doff.assign(b->n + 1, 0);
-            uint64_t total = 0;
-            for (size_t k = 0; k < b->n; ++k) {
-                b->claim[k] = tdt_claimed_size(b->mem.data() + b->off[k], b->off[k + 1] - b->off[k]);
-                if (b->claim[k] > 0 && b->claim[k] <= (int64_t)lim) total += (uint64_t)b->claim[k];
-            }
-            b->dec.reserve(std::max<uint64_t>(total, 1));
             try {
+                b->claim.resize(b->n);
+                b->st.assign(b->n, TDT_OK);
+                b->doff.assign(b->n + 1, 0);
+                uint64_t total = 0;
+                for (size_t k = 0; k < b->n; ++k) {
+                    b->claim[k] = tdt_claimed_size(b->mem.data() + b->off[k], b->off[k + 1] - b->off[k]);
+                    if (b->claim[k] > 0 && b->claim[k] <= (int64_t)lim) total += (uint64_t)b->claim[k];
+                }
+                b->dec.reserve(std::max<uint64_t>(total, 1));
                 // runs of frames within the limit: one decode call each (a frame claiming more is
                 // never decoded: TDT_E_CAPACITY, no payload)
                 uint64_t o = 0;

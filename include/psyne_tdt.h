@@ -163,8 +163,9 @@ int tdt_analyze_batch(tdt_ctx *ctx, const uint8_t *d_in, const uint64_t *d_in_of
                       uint32_t *d_hist, double *d_entropy, int32_t *d_mapping, int32_t *d_status,
                       void *hip_stream);
 
-/* Host-memory path (the TCP socket-buffer case).  The batch runs as 64 MiB chunks on two
- * streams (H2D, kernel and D2H of neighbouring chunks overlap).  Pinned caller buffers are DMA'd
+/* Host-memory path (the TCP socket-buffer case).  The batch runs as chunks (an eighth of the
+ * call's input, 2-64 MiB) through four pipeline slots, each its own stream: H2D, kernel and D2H of
+ * neighbouring chunks overlap.  Pinned caller buffers are DMA'd
  * directly; pageable ones (std::vector, numpy) are staged through the context's pinned buffers
  * by a pool of host threads (TDT_OPT_COPY_THREADS).  h_out must hold the sum of
  * tdt_encode_bound (encode) or of the decoded sizes (decode); h_out_off receives n+1 offsets.

@@ -4,7 +4,10 @@
 //   * a 24-byte TDT frame whose header claims original_size = 0xFFFFFFF0 is rejected BEFORE
 //     decoding ("TDT: decoded message larger than the buffer"), and the connection stays usable;
 //   * in receive_batch one oversized frame gets TDT_E_CAPACITY while its neighbours decode;
-//   * reference decode errors keep the reference's text ("Invalid TDT magic number").
+//   * reference decode errors keep the reference's text ("Invalid TDT magic number");
+//   * after receive_batch started the pipeline with a small max_msg, a frame larger than its
+//     buffers (and than the decoder's limit) still reaches transport_receive intact (ADVICE r04:
+//     the receiver used to hand Inner a too-small buffer, which drops the connection).
 // Prints "cpp substrate OK" on success.
 #include <psyne_amd/tdt_substrate.hpp>
 
@@ -86,6 +89,20 @@ int main() {
     CHECK(off[1] - off[0] == msg.size() && std::memcmp(out.data() + off[0], msg.data(), msg.size()) == 0, "batch 0");
     CHECK(off[2] == off[1], "batch 1 empty");
     CHECK(off[3] - off[2] == m2.size() && std::memcmp(out.data() + off[2], m2.data(), m2.size()) == 0, "batch 2");
+
+    // 4b. a frame larger than the pipeline's buffers and its decoder's limit (64 KiB above),
+    //     then a small one: both arrive, the connection stays up
+    std::vector<uint8_t> big = grad(rng, 131072);  // 512 KiB payload, ~410 KB frame
+    std::vector<uint8_t> bigb = rx.codec().encode(big.data(), big.size());
+    raw.transport_send(bigb.data(), bigb.size());
+    raw.transport_send(b2.data(), b2.size());
+    rx.transport_receive(buf.data(), buf.size());
+    CHECK(rx.last_received_size() == big.size() && std::memcmp(buf.data(), big.data(), big.size()) == 0,
+          "large frame after a small receive_batch");
+    rx.transport_receive(buf.data(), buf.size());
+    CHECK(rx.last_received_size() == m2.size() && std::memcmp(buf.data(), m2.data(), m2.size()) == 0,
+          "frame after the large one");
+    CHECK(rx.inner().is_connected(), "connection kept");
 
     // 5. default construction (ChannelBridge: std::make_unique<SubstrateType>())
     static_assert(std::is_default_constructible_v<TdtSubstrate<PosixTcpSubstrate>>);

@@ -154,7 +154,9 @@ def test_capture_on_cold_context_is_refused():
 
 def test_batches_of_other_shapes_on_a_warm_context():
     """Grids come from the previous batch's counts: a following batch with more small, medium
-    and large messages runs through the overflow launches and must be exact."""
+    and large messages runs through the overflow launches and must be exact.  Every blob of
+    every shape is compared with the oracle (round 4 sampled 40: its r04_k1 failure showed only
+    as a round-trip mismatch)."""
     from oracle.oracle import Oracle
     orc = Oracle()
     codec = _codec()
@@ -170,8 +172,9 @@ def test_batches_of_other_shapes_on_a_warm_context():
         s.run()
         torch.cuda.synchronize()
         got = s.blobs()
-        for i in rng.choice(len(msgs), min(len(msgs), 40), replace=False):
-            assert got[i] == orc.encode(msgs[i], cfg=orc.config(sample_fraction=1.0), bandwidth=10.0), (k, i)
+        cfg = orc.config(sample_fraction=1.0)
+        bad = [i for i in range(len(msgs)) if got[i] != orc.encode(msgs[i], cfg=cfg, bandwidth=10.0)]
+        assert not bad, (k, len(bad), bad[:8])
         assert torch.equal(s.dec[: data.numel()], data), k
         assert int(s.est.abs().sum()) == 0 and int(s.dst.abs().sum()) == 0
     assert codec.error_flags() == 0

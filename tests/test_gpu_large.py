@@ -269,3 +269,44 @@ def test_count_list_history_on_warm_context():
     runs = [runs_message(rng, (1 << 20) + 4 * 77, 300) for _ in range(5)]
     for batch in (grads, runs, grads, grads + runs[:2] + [np.zeros(3 << 20, np.uint8)], runs):
         check_batch(batch, codec=codec)
+
+
+def gradient64(rng, n):
+    """float64 gradients (70 % zeros): six high-entropy mantissa bytes and two low-entropy
+    sign / exponent bytes per word, so word size 8 takes the speculated mapping 0x3f."""
+    x = rng.normal(0, 0.01, n // 8)
+    x[rng.random(x.size) < 0.7] = 0
+    return x.view(np.uint8)
+
+
+@pytest.mark.timeout(300)
+def test_speculated_mapping_ws8():
+    """Word size 8 messages whose mapping IS the speculated [1,1,1,1,1,1,0,0] (the
+    ws=8 tests used float32 data, which never produces it): streaming messages (64 KiB up to the
+    tile threshold) and tiled ones (above it), every blob against the oracle."""
+    rng = np.random.default_rng(88)
+    msgs = [gradient64(rng, 96 * 1024), gradient64(rng, 200 * 1024), gradient64(rng, 1 << 20),
+            gradient64(rng, (3 << 20) + 8 * 77), gradient64(rng, 16 * 1024)]
+    orc = Oracle()
+    for m in msgs[:3]:  # (the premise: the speculated mapping is the real one)
+        b = orc.encode(m, cfg=orc.config(word_size=8), bandwidth=10.0)
+        assert list(np.frombuffer(b[20:52], np.int32)) == [1, 1, 1, 1, 1, 1, 0, 0]
+    check_batch(msgs, ws=8)
+
+
+@pytest.mark.timeout(300)
+def test_speculated_tile_recount():
+    """A word size 4 gradient above the tile threshold with a long constant stretch: its mapping
+    is the speculated one, but the tiles holding the stretch cannot rule the 255-cap out and are
+    counted again (kRecount) — the branch ADVICE r04 found untested."""
+    rng = np.random.default_rng(44)
+    m = gradient(rng, 2 << 20)
+    f = m.view(np.float32)
+    f[100000:100000 + 60000] = np.float32(0.5)      # 240 KB of one nonzero value: runs >> 255
+    f[300000:300003] = np.float32(-0.25)
+    m2 = gradient(rng, (1 << 20) + 4096)
+    m2.view(np.float32)[5000:9000] = np.float32(1e-3)
+    orc = Oracle()
+    b = orc.encode(m, cfg=orc.config(), bandwidth=10.0)
+    assert list(np.frombuffer(b[20:36], np.int32)) == [1, 1, 1, 0]
+    check_batch([m, m2, gradient(rng, 512 * 1024)])
