@@ -66,6 +66,8 @@ def parse():
                     help="also time host buffers (pinned and pageable) through H2D+kernel+D2H")
     ap.add_argument("--latency", action="store_true",
                     help="also time one message per call (1 KiB / 64 KiB / 1 MiB) against the reference CPU codec")
+    ap.add_argument("--latency-sizes", default="1024,65536,1048576",
+                    help="message sizes of the --latency rows (comma-separated bytes)")
     ap.add_argument("--compacted-steps", type=int, default=3,
                     help="timed steps of the compacted (look-back) API leg after the headline (0 = skip)")
     ap.add_argument("--seed", type=int, default=None)
@@ -723,7 +725,8 @@ def main():
     if a.host_inclusive and a.workload != "c4":
         host = host_inclusive(torch, codec, data, off, n, mb)
         host["pcie_ceiling"] = pcie_ceiling(torch, dev)
-    latency = message_latency(torch, codec, data) if a.latency and rank == 0 else None
+    latency = (message_latency(torch, codec, data, sizes=[int(x) for x in a.latency_sizes.split(",")])
+               if a.latency and rank == 0 else None)
     per_rank = gather_obj({"rank": rank, "device": my_dev, "numa": numa, "msgs": n, "payload_bytes": payload,
                            "GiBps": round(my_rate, 3), "kernels_ms": [round(t_enc, 4), round(t_dec, 4)],
                            "host_inclusive": host}, world)

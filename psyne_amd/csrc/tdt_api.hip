@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
@@ -185,8 +186,6 @@ struct tdt_ctx {
     uint8_t *one = nullptr;
     size_t one_bytes = 0;
     hipStream_t one_stream = nullptr;
-    uint8_t *one_dev = nullptr;  // device copy of a larger blob (one-wave decode reads it from HBM)
-    size_t one_dev_bytes = 0;
     std::shared_ptr<CopyPool> pool;  // host threads of the staging copies (shared: tdt_host_copy)
     uint64_t *hbases = nullptr;      // host_encode: device-side running output base per chunk
     size_t hbases_n = 0;
@@ -208,6 +207,10 @@ struct tdt_ctx {
     bool small_main = false;    // PSYNE_TDT_SMALL_MAIN: small lists on the caller's stream
     bool no_two_phase = false;  // PSYNE_TDT_NO_TWO_PHASE: compacted calls take the one-pass kernels
     bool no_one = false;        // PSYNE_TDT_NO_ONE: one-message host calls take the pipeline too
+    bool one_wave = false;      // PSYNE_TDT_ONE_WAVE=1: one-message decode as one wave (round-4 path)
+    uint64_t one_wave_max = 4096;  // one-message decode: outputs up to this size take the one-wave kernel
+    bool one_spin = true;       // PSYNE_TDT_ONE_SPIN=0: one-message calls wait in hipStreamSynchronize
+    uint32_t one_seq = 0;
     uint32_t copy_wgs = 8;      // PSYNE_TDT_COPY_WGS: copy-list workgroups per CU
     // PSYNE_TDT_DSMALL_MAX: blobs decoding to at most this many bytes take the one-round-window
     // list on the side stream (C4 decode 11.80 -> 11.42 ms at 8 KiB against 1 KiB; 16-64 KiB
@@ -1472,13 +1475,13 @@ int host_decode(tdt_ctx *c, const uint8_t *h_in, const uint64_t *h_in_off, uint3
 // memory the kernel reads and writes over PCIe.
 constexpr uint64_t kOneMax = 256 * 1024;  // largest message (encode) / decoded message the path takes
 constexpr size_t kOneIn = 256;
-constexpr uint64_t kOneDevMin = 16 * 1024;  // decode: blobs above this are copied to HBM first
 struct OneArgs {
     uint64_t off[2];   // input offsets
     uint64_t slot[2];  // output slot
     uint64_t len;      // output length
     int32_t status;
     uint32_t list, cnt, flags;
+    uint32_t done, pad;  // completion word (one_spin: written by the stream after the kernel)
 };
 
 int ensure_one(tdt_ctx *c, size_t bytes) {
@@ -1539,6 +1542,7 @@ int host_one(tdt_ctx *c, bool encode, const uint8_t *h_in, const uint64_t *h_in_
     A->list = 0;
     A->cnt = 1;
     A->flags = 0;
+    A->done = 0;
     if (len) std::memcpy(hb + kOneIn, src, len);
     hipStream_t s = c->one_stream;
     if (encode) {
@@ -1570,19 +1574,9 @@ int host_one(tdt_ctx *c, bool encode, const uint8_t *h_in, const uint64_t *h_in_
     } else {
         psy::DecodeArgs a{};
         a.in = db + kOneIn;
-        if (len > kOneDevMin) {
-            // one wave walks the blob window by window: its pair loads are dependent, so they come
-            // from HBM (one DMA of the blob) rather than over PCIe one window at a time
-            if (len > c->one_dev_bytes) {
-                if (c->one_dev) HIPCHK(hipFree(c->one_dev));
-                c->one_dev = nullptr;
-                c->one_dev_bytes = 0;
-                HIPCHK(hipMalloc(&c->one_dev, std::max<size_t>(len, 256 * 1024)));
-                c->one_dev_bytes = std::max<size_t>(len, 256 * 1024);
-            }
-            HIPCHK(hipMemcpyAsync(c->one_dev, hb + kOneIn, len, hipMemcpyHostToDevice, s));
-            a.in = c->one_dev;
-        }
+        // (blobs are read in place over PCIe: staging them into HBM first, in the kernel or by a
+        // copy, measured no faster — profiles/r05_diag/one_message/)
+        const bool one_wave = c->one_wave || osize <= c->one_wave_max;
         a.in_off = dA->off;
         a.n_msgs = 1;
         a.out = db + o_out;
@@ -1592,10 +1586,30 @@ int host_one(tdt_ctx *c, bool encode, const uint8_t *h_in, const uint64_t *h_in_
         a.errflags = const_cast<uint32_t *>(&dA->flags);
         a.list = &dA->list;
         a.list_count = &dA->cnt;
-        hipLaunchKernelGGL((psy::tdt_decode_kernel<0, psy::kDecWR, 0>), dim3(1), dim3(64), 0, s, a);
+        if (one_wave)
+            hipLaunchKernelGGL((psy::tdt_decode_kernel<0, psy::kDecWR, 0>), dim3(1), dim3(64), 0, s, a);
+        else  // a workgroup of kOneWaves waves: tiles of the blob (tdt_decode_one_kernel)
+            hipLaunchKernelGGL((psy::tdt_decode_one_kernel<psy::kOneWaves>), dim3(1), dim3(64 * psy::kOneWaves), 0,
+                               s, a);
     }
     HIPCHK(hipGetLastError());
-    HIPCHK(hipStreamSynchronize(s));
+    bool done = false;
+    if (c->one_spin) {
+        // the stream writes `done` after the kernel; the host spins on it (1 ms at most, then the
+        // stream sync, which also reports a failed kernel)
+        const uint32_t seq = ++c->one_seq ? c->one_seq : ++c->one_seq;
+        HIPCHK(hipStreamWriteValue32(s, const_cast<uint32_t *>(&dA->done), seq, 0));
+        const auto t0 = std::chrono::steady_clock::now();
+        for (uint32_t k = 1;; ++k) {
+            if (__atomic_load_n(&A->done, __ATOMIC_ACQUIRE) == seq) {
+                done = true;
+                break;
+            }
+            __builtin_ia32_pause();
+            if ((k & 255) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(1)) break;
+        }
+    }
+    if (!done) HIPCHK(hipStreamSynchronize(s));
     c->host_flags.fetch_or(A->flags);
     const uint64_t olen = A->len;
     const int32_t ost = A->status;
@@ -1721,6 +1735,8 @@ int tdt_ctx_create(int device, const tdt_config *cfg, tdt_ctx **out) {
     x->small_main = flag("PSYNE_TDT_SMALL_MAIN");
     x->no_two_phase = flag("PSYNE_TDT_NO_TWO_PHASE");
     x->no_one = flag("PSYNE_TDT_NO_ONE");
+    x->one_wave = flag("PSYNE_TDT_ONE_WAVE");
+    if (const char *e = std::getenv("PSYNE_TDT_ONE_SPIN")) x->one_spin = *e == '1';
     if (const char *e = std::getenv("PSYNE_TDT_DBIG_MIN")) x->dbig_min = std::strtoull(e, nullptr, 10);
     if (const char *e = std::getenv("PSYNE_TDT_DSMALL_MAX")) x->dsmall_max = std::strtoull(e, nullptr, 10);
     if (const char *e = std::getenv("PSYNE_TDT_COPY_WGS")) x->copy_wgs = std::max(1ul, std::strtoul(e, nullptr, 10));
@@ -1750,7 +1766,6 @@ void tdt_ctx_destroy(tdt_ctx *ctx) {
     if (ctx->hbases) (void)hipFree(ctx->hbases);
     if (ctx->one_stream) (void)hipStreamSynchronize(ctx->one_stream);
     if (ctx->one) (void)hipHostFree(ctx->one);
-    if (ctx->one_dev) (void)hipFree(ctx->one_dev);
     if (ctx->one_stream) (void)hipStreamDestroy(ctx->one_stream);
     if (ctx->astream) (void)hipStreamSynchronize(ctx->astream);
     if (ctx->h_dev) (void)hipFree(ctx->h_dev);

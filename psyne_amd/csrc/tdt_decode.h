@@ -1421,6 +1421,123 @@ __global__ __launch_bounds__(64) void tdt_decode_ltile_kernel(DecodeArgs a) {
     }
 }
 
+// One blob, one workgroup of NW waves (the one-message host call, tdt_decode_host with a single
+// blob, protocol_demo.cpp:164-189's per-message decode): the large-blob passes — block sums
+// (lblock), their scan (lscan), output tiles through decode_fast (ltile) — in ONE launch with
+// the scan in LDS, so a 64 KiB blob is NW waves' tiles, not one wave walking 64 rounds with a
+// dependent block load per window.  Every wave parses the header itself (no broadcast); any
+// shape decode_fast does not take (UNCP, generic, errors) goes to wave 0's decode_one.
+constexpr int kOneWaves = 16;
+constexpr uint32_t kOneBlocks = 640;  // block sums in LDS (the host caps the blob at ~514 blocks)
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void tdt_decode_one_kernel(DecodeArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t smem[NW][DecLayout::BYTES];
+    __shared__ uint32_t s_bs[kOneBlocks];  // block sums, then (scan) block start positions
+    __shared__ uint32_t s_slen[2];
+    const uint32_t w = threadIdx.x >> 6, lane = (uint32_t)lane_id();
+    const uint64_t boff = a.in_off[0];
+    const uint64_t len = a.in_off[1] - boff;
+    const uint8_t *blob = a.in + boff;
+    uint8_t *hdrc = smem[w] + DecLayout::OFF_HDR;
+    {
+        const uint64_t hc = len < (uint64_t)kHdrCache ? len : (uint64_t)kHdrCache;
+        const uint32_t o = lane * 4u;
+        uint32_t v = 0;
+        if (((uintptr_t)blob & 3) == 0 && o + 4 <= hc) {
+            v = *reinterpret_cast<const uint32_t *>(blob + o);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                if (o + i < hc) v |= (uint32_t)blob[o + i] << (8 * i);
+        }
+        reinterpret_cast<uint32_t *>(hdrc)[lane] = v;
+    }
+    team_sync<1>();
+    const uint32_t hcl = len < (uint64_t)kHdrCache ? (uint32_t)len : (uint32_t)kHdrCache;
+    const FastHdr H = parse_fast(blob, len, hdrc, hcl);
+    const uint32_t nb0 = (H.np[0] + 511u) / 512u, nb1 = H.two ? (H.np[1] + 511u) / 512u : 0u;
+    // (H is the same in every wave: these branches are workgroup-uniform)
+    if (H.kind != 2 || nb0 + nb1 > kOneBlocks) {
+        if (w == 0) {
+            team_sync<1>();  // (the header cache is decode_one's to refill)
+            decode_one<0>(a, smem[0], 0);
+        }
+        return;
+    }
+    const uint64_t ob = a.slot_off[0];
+    const bool fits = H.osize <= a.slot_off[1] - ob;
+    if (w == 0 && lane == 0) {
+        if (a.out_len) a.out_len[0] = fits ? H.osize : 0;
+        if (a.status) a.status[0] = fits ? ST_OK : ST_CAPACITY;
+    }
+    if (!fits) return;
+    uint8_t *dst = a.out + ob;
+    const uint64_t wbytes = (uint64_t)(H.orig / H.ws) * H.ws;
+    if (w == 0 && H.orig > wbytes) team_zero<64>(dst + wbytes, H.orig - wbytes);
+    // ---- block sums (lblock): wave w takes blocks w, w + NW, ...
+    for (uint32_t b = w; b < nb0 + nb1; b += NW) {
+        const uint32_t r = b < nb0 ? 0u : 1u;
+        const uint32_t np = H.np[r], soff = H.soff[r];
+        const uint32_t p0 = 512u * (r ? b - nb0 : b) + 8u * lane;
+        const uint32_t nv = p0 < np ? (np - p0 < 8u ? np - p0 : 8u) : 0u;
+        const uint4 pv = nv ? ld16_span(blob + soff + 2ull * p0, (int)(2 * nv), blob + len) : make_uint4(0, 0, 0, 0);
+        const uint32_t s2 = (pv.x & 0x00ff00ffu) + (pv.y & 0x00ff00ffu) + (pv.z & 0x00ff00ffu) + (pv.w & 0x00ff00ffu);
+        const uint32_t tot = wave_reduce<OpAdd>((s2 & 0xffffu) + (s2 >> 16));
+        if (lane == 0) s_bs[b] = tot;
+    }
+    __syncthreads();
+    // ---- scan (lscan): wave r, stream r's block sums → start positions, in place
+    if (w < (H.two ? 2u : 1u)) {
+        const uint32_t n = w ? nb1 : nb0, base = w ? nb0 : 0u;
+        uint32_t run = 0;
+        for (uint32_t c0 = 0; c0 < n; c0 += 64) {
+            const uint32_t b = c0 + lane;
+            const uint32_t v = b < n ? s_bs[base + b] : 0u;
+            const uint32_t incl = wave_incl_scan<OpAdd>(v);
+            if (b < n) s_bs[base + b] = run + incl - v;
+            run += rdlane(incl, 63);
+        }
+        if (lane == 0) s_slen[w] = run;
+    }
+    __syncthreads();
+    // ---- tiles (ltile): wave w decodes tiles w, w + NW, ... of TG groups (whole rounds)
+    const uint32_t ngroups = (uint32_t)((wbytes + 15) / 16);
+    const uint32_t TG = ((ngroups + NW - 1) / NW + 63u) & ~63u;
+    const uint32_t nt = (ngroups + TG - 1) / TG;
+    for (uint32_t t = w; t < nt; t += NW) {
+        if (t != w) team_sync<1>();
+        const uint32_t g_lo = t * TG, g_hi = ngroups - g_lo < TG ? ngroups : g_lo + TG;
+        uint32_t b0[2] = {0u, 0u}, s0[2] = {0u, 0u};
+        if (g_lo > 0) {
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                if (r == 1 && !H.two) break;
+                const uint32_t P1 = g_lo * H.seg[r] - 1u, slen = s_slen[r];
+                const uint32_t n = r ? nb1 : nb0, base = r ? nb0 : 0u;
+                if (P1 >= slen) {  // the stream ended before this tile: zeros
+                    b0[r] = kNone;
+                    s0[r] = slen;
+                    continue;
+                }
+                // the block holding position P1: start <= P1 < the next block's start
+                for (uint32_t c0 = 0; c0 < n; c0 += 64) {
+                    const uint32_t b = c0 + lane;
+                    const uint32_t st = b < n ? s_bs[base + b] : ~0u;
+                    const uint32_t en = b + 1 < n ? s_bs[base + b + 1] : slen;
+                    const uint64_t hit = __ballot(b < n && st <= P1 && P1 < en);
+                    if (hit) {
+                        const uint32_t bl = (uint32_t)__builtin_ctzll(hit);
+                        b0[r] = c0 + bl;
+                        s0[r] = rdlane(st, (int)bl);
+                        break;
+                    }
+                }
+            }
+        }
+        decode_fast(H, smem[w], blob, blob + len, dst, ngroups, wbytes, g_lo, g_hi, b0, s0);
+    }
+}
+
 // Blob ids: the look-back needs them in dispatch order (atomic ticket); slotted batches take
 // them from the plan's list (or, without one, the workgroup id).
 // List entries are bounded by the plan's device-side count (main launch: one blob per wave over

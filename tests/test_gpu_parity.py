@@ -2,6 +2,7 @@
 reference codec, and against the CPU oracle on seeded inputs.  Bit-exact everywhere: this
 is byte/integer work (the only floating point, the entropy decision, is restated
 bit-exactly; tests/test_log2_restatement.py)."""
+import pathlib
 import struct
 
 import numpy as np
@@ -588,6 +589,61 @@ def test_one_message_host_path(orc, ws):
         b = np.frombuffer(bad, np.uint8)
         dec, doff, dst = codec.decode_host(b, np.array([0, b.size], np.uint64), 64)
         assert int(dst[0]) == code and int(doff[1]) == 0
+    assert codec.error_flags() == 0
+
+
+def _runs(rng, n, mean_run, alphabet=4):
+    out = np.empty(n, np.uint8)
+    i = 0
+    while i < n:
+        L = int(rng.geometric(1.0 / mean_run))
+        out[i:i + L] = rng.integers(0, alphabet)
+        i += L
+    return out
+
+
+@pytest.mark.parametrize("env", [{}, {"PSYNE_TDT_ONE_SPIN": "0"}, {"PSYNE_TDT_ONE_WAVE": "1"}],
+                         ids=["tiles", "tiles_sync", "one_wave"])
+def test_one_message_decode_tiles(orc, env, monkeypatch):
+    """The one-message decode (tdt_decode_one_kernel: block sums, their scan in LDS and 16 waves'
+    output tiles in one launch) on blobs whose runs cross every tile boundary, whose streams end
+    before the output does (zeros), hold count-0 pairs or one empty stream, and on the shapes it
+    hands to wave 0's decode_one (UNCP, a ws-8 generic mapping, truncated blobs): statuses and
+    bytes equal the oracle's.  Completion seen by the spin on the stream-written word or by the
+    stream sync, and the round-4 one-wave kernel, give the same results."""
+    import sys
+    sys.path.insert(0, str(pathlib.Path(__file__).resolve().parent))
+    from test_gpu_large import build_blob, parse_blob
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    rng = np.random.default_rng(131)
+    codec = make_codec()
+    cfg = orc.config(sample_fraction=1.0)
+    blobs = []
+    for n, mr in ((65536, 0), (262144, 0), (262144, 300), (200000, 40), (131072, 5000), (4096, 0), (65536 + 16, 900)):
+        m = grad(rng, n // 4) if mr == 0 else _runs(rng, n, mr)
+        blobs.append(orc.encode(np.ascontiguousarray(m), cfg=cfg, bandwidth=10.0))
+    w, mp, streams = parse_blob(blobs[1])
+    assert len(streams) == 2
+    blobs.append(build_blob(w, mp, [streams[0], streams[1][: (len(streams[1]) // 6) * 2]]))  # stream 1 short
+    blobs.append(build_blob(w, mp, [streams[0][:(len(streams[0]) // 3) * 2], streams[1]]))  # stream 0 short
+    blobs.append(build_blob(w, mp, [b"", streams[1]]))  # stream 0 empty
+    s0 = bytearray(streams[0])
+    for k in range(0, len(s0) - 1, 2 * 211):
+        s0[k] = 0
+    blobs.append(build_blob(w, mp, [bytes(s0), streams[1]]))  # count-0 pairs
+    blobs.append(blobs[1][:-7])  # truncated
+    x = grad(rng, 32768)
+    blobs.append(orc.encode(x, cfg=orc.config(word_size=8, sample_fraction=1.0), bandwidth=10.0,
+                            mapping=[1, 1, 1, 0, 0, 0, 0, 0]))  # generic shape (ws 8)
+    blobs.append(orc.encode(rng.integers(0, 256, 100001, dtype=np.uint8), cfg=cfg, bandwidth=10.0))  # UNCP
+    for i, b in enumerate(blobs):
+        arr = np.frombuffer(b, np.uint8).copy()
+        ost, want = orc.decode(b)
+        dec, doff, dst = codec.decode_host(arr, np.array([0, arr.size], np.uint64), 1 << 18)
+        assert int(dst[0]) == ost, "blob %d (%d B) status %d vs oracle %d" % (i, arr.size, dst[0], ost)
+        if ost == 0:
+            assert dec.tobytes() == want, "blob %d (%d B) bytes" % (i, arr.size)
     assert codec.error_flags() == 0
 
 
