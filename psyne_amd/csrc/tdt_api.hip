@@ -177,6 +177,7 @@ struct tdt_ctx {
         uint8_t *stage_in = nullptr, *stage_out = nullptr;  // pinned staging for pageable callers
         size_t sin_bytes = 0, sout_bytes = 0;
         hipEvent_t evc = nullptr;  // after the chunk's output copy (orders the next chunk's)
+        hipEvent_t evi = nullptr;  // after the chunk's input copy (orders the next chunk's)
         PlanWS pw;
     } hs[kHostSlots];
     // one-message fast path (tdt_encode_host / tdt_decode_host with one message of at most
@@ -208,7 +209,9 @@ struct tdt_ctx {
     bool no_two_phase = false;  // PSYNE_TDT_NO_TWO_PHASE: compacted calls take the one-pass kernels
     bool no_one = false;        // PSYNE_TDT_NO_ONE: one-message host calls take the pipeline too
     bool one_wave = false;      // PSYNE_TDT_ONE_WAVE=1: one-message decode as one wave (round-4 path)
-    uint64_t one_wave_max = 4096;  // one-message decode: outputs up to this size take the one-wave kernel
+    uint64_t one_wave_max = 4096;
+    bool dout_sdma = false;     // PSYNE_TDT_DOUT_SDMA=1: host_decode's output by hipMemcpyAsync (round 4)
+    bool h2d_order = true;      // PSYNE_TDT_H2D_ORDER=0: host_decode chunks' input copies unordered (round 4)  // one-message decode: outputs up to this size take the one-wave kernel
     bool one_spin = true;       // PSYNE_TDT_ONE_SPIN=0: one-message calls wait in hipStreamSynchronize
     uint32_t one_seq = 0;
     uint32_t copy_wgs = 8;      // PSYNE_TDT_COPY_WGS: copy-list workgroups per CU
@@ -984,6 +987,7 @@ int ensure_slot(tdt_ctx *c, int k, size_t dev_bytes, size_t pin_words, size_t si
         HIPCHK(hipStreamCreateWithFlags(&h.stream, hipStreamNonBlocking));
         HIPCHK(hipEventCreateWithFlags(&h.ev, hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&h.evc, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&h.evi, hipEventDisableTiming));
         HIPCHK(hipHostMalloc(&h.flag, 4, hipHostMallocDefault));
         *h.flag = 0;
     }
@@ -1129,14 +1133,9 @@ __device__ __forceinline__ void wave_copy_any(uint8_t *dst, const uint8_t *src, 
 // chunk's launch, which this one follows by an event).  Past out_cap nothing is copied (the host
 // reports TDT_E_CAPACITY).  Stores are 16-byte aligned on dst; the source is read as aligned
 // dwords and funnel-shifted.
-__global__ __launch_bounds__(256) void host_out_kernel(const uint8_t *src, const uint64_t *chunk_off, uint32_t n,
-                                                       uint8_t *dst, uint64_t *bases, uint32_t ci, uint64_t cap,
-                                                       int direct) {
-    const uint64_t total = chunk_off[n];
-    const uint64_t base = bases[ci];
-    if (blockIdx.x == 0 && threadIdx.x == 0) bases[ci + 1] = base + total;
-    if (base + total > cap || total == 0) return;
-    uint8_t *d = direct ? dst + base : dst;
+// total bytes src → d (host memory over PCIe, or device): 16-byte stores at d's alignment, the
+// source read as aligned dwords and shifted (src + total + 4 must be readable)
+__device__ __forceinline__ void grid_copy_out(uint8_t *d, const uint8_t *src, uint64_t total) {
     const uint64_t gtid = (uint64_t)blockIdx.x * 256 + threadIdx.x, gsz = (uint64_t)gridDim.x * 256;
     uint64_t head = (16 - ((uintptr_t)d & 15)) & 15;
     if (head > total) head = total;
@@ -1154,6 +1153,21 @@ __global__ __launch_bounds__(256) void host_out_kernel(const uint8_t *src, const
                            (uint32_t)((((uint64_t)w3 << 32) | w2) >> sh), (uint32_t)((((uint64_t)w4 << 32) | w3) >> sh));
     }
     for (uint64_t k = head + 16 * nb + gtid; k < total; k += gsz) d[k] = src[k];
+}
+
+__global__ __launch_bounds__(256) void host_out_kernel(const uint8_t *src, const uint64_t *chunk_off, uint32_t n,
+                                                       uint8_t *dst, uint64_t *bases, uint32_t ci, uint64_t cap,
+                                                       int direct) {
+    const uint64_t total = chunk_off[n];
+    const uint64_t base = bases[ci];
+    if (blockIdx.x == 0 && threadIdx.x == 0) bases[ci + 1] = base + total;
+    if (base + total > cap || total == 0) return;
+    grid_copy_out(direct ? dst + base : dst, src, total);
+}
+
+// host_decode: a chunk's slotted output → the caller's pinned buffer (or the pinned staging)
+__global__ __launch_bounds__(256) void host_dout_kernel(const uint8_t *src, uint8_t *dst, uint64_t total) {
+    grid_copy_out(dst, src, total);
 }
 
 // A slotted chunk's blob lengths → exclusive offsets (total at [n]): one workgroup, 4096
@@ -1389,6 +1403,13 @@ int host_decode(tdt_ctx *c, const uint8_t *h_in, const uint64_t *h_in_off, uint3
     }
     if (need > out_cap) return set_err(TDT_E_CAPACITY, "host output capacity exceeded");
     const bool pin_in = is_pinned(h_in + h_in_off[0]), pin_out = is_pinned(h_out);
+    // the device's view of a pinned caller buffer (registered memory may map elsewhere)
+    uint8_t *d_hout = nullptr;
+    if (pin_out && hipHostGetDevicePointer(reinterpret_cast<void **>(&d_hout), h_out, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        d_hout = nullptr;
+    }
+    const bool dma_out = c->dout_sdma || (pin_out && !d_hout);
     std::vector<Chunk> ch;
     uint64_t base = 0;
     const uint64_t cb = host_chunk_bytes(h_in_off, n_msgs);
@@ -1426,15 +1447,28 @@ int host_decode(tdt_ctx *c, const uint8_t *h_in, const uint64_t *h_in_off, uint3
         auto *dslot = doff + (k.n + 1);
         auto *dst = reinterpret_cast<int32_t *>(d + k.o_st);
         auto *dlen = reinterpret_cast<uint64_t *>(d + k.o_len);
+        // input copies in chunk order, each after the previous chunk's: concurrent copies of
+        // several slots share the link and all land late, the earliest-needed one included
+        // (decode 31 -> 37 GiB/s pinned; the same ordering cost host_encode 44 -> 36 GiB/s,
+        // profiles/r05_diag/host_decode/)
+        if (ci > 0 && c->h2d_order) HIPCHK(hipStreamWaitEvent(h.stream, c->hs[(ci - 1) % kHostSlots].evi, 0));
         HIPCHK(hipMemcpyAsync(d, src, k.in_bytes, hipMemcpyHostToDevice, h.stream));
+        HIPCHK(hipEventRecord(h.evi, h.stream));
         HIPCHK(hipMemcpyAsync(doff, pin_in_off, 16ull * (k.n + 1), hipMemcpyHostToDevice, h.stream));  // offsets + slots
         st = decode_common(c, false, d, doff, k.n, d + k.o_out, 0, nullptr, nullptr, dst, h.stream, dslot, dlen,
                            nullptr, d + k.o_ws, &h.pw);
         if (st) return st;
         HIPCHK(hipMemcpyAsync(h.flag, d + k.o_ws + 4, 4, hipMemcpyDeviceToHost, h.stream));
-        if (acc)
+        if (acc && dma_out) {
             HIPCHK(hipMemcpyAsync(pin_out ? h_out + k.base : h.stage_out, d + k.o_out, acc, hipMemcpyDeviceToHost,
                                   h.stream));
+        } else if (acc) {
+            // the output crosses PCIe as a copy kernel's stores (as host_encode's), not a DMA: the
+            // DMA engines then carry only the H2D direction
+            hipLaunchKernelGGL(host_dout_kernel, dim3((uint32_t)std::min<uint64_t>(1024, acc / 4096 + 1)), dim3(256), 0,
+                               h.stream, d + k.o_out, pin_out ? d_hout + k.base : h.stage_out, acc);
+            HIPCHK(hipGetLastError());
+        }
         HIPCHK(hipMemcpyAsync(pin_back(h, k), dlen, 8ull * k.n, hipMemcpyDeviceToHost, h.stream));
         HIPCHK(hipMemcpyAsync(pin_status(h, k), dst, 4ull * k.n, hipMemcpyDeviceToHost, h.stream));
         HIPCHK(hipEventRecord(h.ev, h.stream));
@@ -1736,6 +1770,8 @@ int tdt_ctx_create(int device, const tdt_config *cfg, tdt_ctx **out) {
     x->no_two_phase = flag("PSYNE_TDT_NO_TWO_PHASE");
     x->no_one = flag("PSYNE_TDT_NO_ONE");
     x->one_wave = flag("PSYNE_TDT_ONE_WAVE");
+    x->dout_sdma = flag("PSYNE_TDT_DOUT_SDMA");
+    if (const char *e = std::getenv("PSYNE_TDT_H2D_ORDER")) x->h2d_order = *e == '1';
     if (const char *e = std::getenv("PSYNE_TDT_ONE_SPIN")) x->one_spin = *e == '1';
     if (const char *e = std::getenv("PSYNE_TDT_DBIG_MIN")) x->dbig_min = std::strtoull(e, nullptr, 10);
     if (const char *e = std::getenv("PSYNE_TDT_DSMALL_MAX")) x->dsmall_max = std::strtoull(e, nullptr, 10);
@@ -1780,6 +1816,7 @@ void tdt_ctx_destroy(tdt_ctx *ctx) {
         h.pw.release();
         if (h.ev) (void)hipEventDestroy(h.ev);
         if (h.evc) (void)hipEventDestroy(h.evc);
+        if (h.evi) (void)hipEventDestroy(h.evi);
         if (h.stream) (void)hipStreamDestroy(h.stream);
     }
     delete ctx;

@@ -11,7 +11,7 @@
 // 16-byte groups (lane l ↔ group l).  Per window and referenced stream r (k_r byte positions
 // per word, so 64·WR·WPG·k_r stream positions):
 //   1. pairs, 8 per lane per pair-round, are prefix-summed (in-lane + DPP wave scan) and each
-//      writes a HEAD key ((position mod 16) + 1) << 8 | value at its start position into an
+//      writes a HEAD key (position tag) << 8 | value at its start position into an
 //      LDS array (positions past the window land in a pad slot); the pairs that start in the
 //      window are consumed (a ballot finds the boundary lane, a scalar walk the exact pair);
 //   2. per round, lane l owns 16 consecutive positions of the round's concatenated stream
@@ -70,6 +70,9 @@ constexpr uint32_t kDecTileGroups = 2048;  // large blobs: 32 KiB of output per 
 #define PSY_DEC_WR 3
 #endif
 constexpr int kDecWR = PSY_DEC_WR;  // rounds per window
+#ifndef PSY_DEC_REBASE_LOG2
+#define PSY_DEC_REBASE_LOG2 28  // decode_fast rebases its held pair starts every 2^this positions
+#endif
 constexpr int kHdrCache = 256;
 
 template <int WR = kDecWR>
@@ -78,6 +81,9 @@ struct DecLayoutT {
     // (seg_0 + seg_1 = 16); a round's plane bytes are staged inside the heads of that round
     // (already read by the fill) and zeroed after the gather.
     static constexpr int FHEADS = (WR * 1024 + 32) * 2;
+    // (the fast path's heads start 16 bytes in: the u16 before stream 0's heads is the pad slot
+    // of pairs that start before the window — stream 1's is the last pad slot of stream 0)
+    static constexpr int OFF_FHEADS = 16;
     // Generic path (any shape, up to 16 referenced streams): windows of GWR rounds, its own
     // planes and the lane-0 parser's fields.
     static constexpr int GWR = 1;
@@ -90,7 +96,7 @@ struct DecLayoutT {
     static constexpr int OFF_GPLANES = GHEADS;
     static constexpr int OFF_MISC = OFF_GPLANES + PLANES;
     static constexpr int GBYTES = OFF_MISC + MISC;
-    static constexpr int BYTES = FHEADS > GBYTES ? FHEADS : GBYTES;
+    static constexpr int BYTES = OFF_FHEADS + FHEADS > GBYTES ? OFF_FHEADS + FHEADS : GBYTES;
     static_assert(kHdrCache + 16 <= GHEADS && kHdrCache + 16 <= FHEADS, "header cache inside the heads");
 };
 using DecLayout = DecLayoutT<>;
@@ -228,9 +234,9 @@ __global__ __launch_bounds__(256) void tdt_decode_sizes_kernel(DecodeArgs a) {
 // writes its key at slot min(st - wstart, wlen): pairs outside the window land in the pad
 // slot, so the write is branch-free (3 VALU + 1 ds_write_b16 per pair).
 //
-// Keys are gen << 13 | (pos mod 16 + 1) << 8 | value (a 5-bit tag) with gen = window index
-// mod 8, so the head array is only zeroed every 8 windows: stale keys compare below the
-// current window's seed key (gen << 13 | value) and below every current head.
+// Keys are gen << 13 | (16 + pos mod 16) << 8 | value (a 5-bit tag, 0 = no head) with gen =
+// window index mod 8, so the head array is only zeroed every 8 windows: stale keys compare
+// below the current window's seed key (gen << 13 | value) and below every current head.
 //
 // Fill, per round of 64 groups: lane l owns 16 consecutive positions of the round's two
 // stream planes (stream 0: lanes [0, 4·seg0), stream 1 after); an in-lane u16 prefix max,
@@ -260,7 +266,7 @@ __device__ __forceinline__ void decode_fast(const FastHdr &H, uint8_t *smem, con
     constexpr uint32_t WR = WR_;
     const uint32_t lane = (uint32_t)lane_id();
     PSY_PROF_BEGIN();
-    uint16_t *heads = reinterpret_cast<uint16_t *>(smem + Lay::OFF_HEADS);
+    uint16_t *heads = reinterpret_cast<uint16_t *>(smem + Lay::OFF_FHEADS);
     // (every field is wave-uniform: readfirstlane keeps them in SGPRs)
     auto U = [](uint32_t x) -> uint32_t { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); };
     const bool two = U(H.two) != 0;
@@ -270,7 +276,7 @@ __device__ __forceinline__ void decode_fast(const FastHdr &H, uint8_t *smem, con
     const uint32_t OA[4] = {U(H.OA[0]), U(H.OA[1]), U(H.OA[2]), U(H.OA[3])};
     const uint32_t OB[4] = {U(H.OB[0]), U(H.OB[1]), U(H.OB[2]), U(H.OB[3])};
     const uint32_t wlen[2] = {WR * 64u * seg[0], WR * 64u * seg[1]};
-    const uint32_t hbase[2] = {(uint32_t)Lay::OFF_HEADS, (uint32_t)Lay::OFF_HEADS + 2u * (wlen[0] + 16u)};
+    const uint32_t hbase[2] = {(uint32_t)Lay::OFF_FHEADS, (uint32_t)Lay::OFF_FHEADS + 2u * (wlen[0] + 16u)};
     // round rl's plane bytes go to the heads of round rl of the stream with the larger segment
     // (128·seg >= 1 KiB bytes, 16-byte aligned), which the fill has read by then
     const uint32_t rbig = seg[1] > seg[0] ? 1u : 0u;
@@ -301,13 +307,18 @@ __device__ __forceinline__ void decode_fast(const FastHdr &H, uint8_t *smem, con
     uint32_t bend[2] = {0u, 0u};      // absolute end position of the loaded block
     uint32_t slen[2] = {~0u, ~0u};    // decoded stream length once its last block is loaded
     bool have[2] = {false, false};
-    uint32_t st[2][8];
+    // pair starts are held as st = 2·(start - P0[r]) (signed; P0 = the stream position of group
+    // g_lo, rebased forward every 2^28 positions), with bit 31 set on count-0 pairs; a window's
+    // key address is then med3(st - c, lo, hi): 2 VALU per pair, pairs outside the window (or
+    // without a count) landing on the pad u16 just before or after the stream's heads
+    int32_t P0[2] = {(int32_t)(g_lo * seg[0]), (int32_t)(g_lo * seg[1])};
+    int32_t st[2][8];
     uint32_t kp[2][4];  // packed keys without gen: key(2j) | key(2j+1) << 16
     uint32_t cv[2] = {0u, 0u};  // carry: value of the last plane position of the previous round
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) st[r][i] = ~0u;
+        for (int i = 0; i < 8; ++i) st[r][i] = INT32_MIN;
 #pragma unroll
         for (int j = 0; j < 4; ++j) kp[r][j] = 0u;
     }
@@ -320,20 +331,21 @@ __device__ __forceinline__ void decode_fast(const FastHdr &H, uint8_t *smem, con
         const uint32_t s2 = (pw[0] & 0x00ff00ffu) + (pw[1] & 0x00ff00ffu) + (pw[2] & 0x00ff00ffu) + (pw[3] & 0x00ff00ffu);
         const uint32_t tot = (s2 & 0xffffu) + (s2 >> 16);
         const uint32_t linc = wave_incl_scan<OpAdd>(tot);
-        uint32_t run = bend[r] + linc - tot;
+        // this lane's first start - P0 (P0 % 16 == 0: the low 4 bits are the position mod 16)
+        uint32_t run = bend[r] - (uint32_t)P0[r] + linc - tot;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const uint32_t w = pw[j];
             const uint32_t c0 = w & 0xffu, c1 = (w >> 16) & 0xffu;
-            // key = (pos mod 16 + 1) << 8 | value; value bytes 1 and 3 of the dword
-            const uint32_t k0 = ((((run & 15u) + 1u) << 8) | ((w >> 8) & 0xffu));
+            const uint32_t r0 = run, r1 = run + c0;
+            run = r1 + c1;
             // (pairs past the stream's end were loaded as zero bytes: count 0, no extra test)
-            st[r][2 * j] = c0 != 0u ? run : ~0u;
-            run += c0;
-            const uint32_t k1 = ((((run & 15u) + 1u) << 8) | (w >> 24));
-            st[r][2 * j + 1] = c1 != 0u ? run : ~0u;
-            run += c1;
-            kp[r][j] = k0 | (k1 << 16);
+            st[r][2 * j] = (int32_t)((r0 << 1) | ((c0 + 0xffffffffu) & 0x80000000u));
+            st[r][2 * j + 1] = (int32_t)((r1 << 1) | ((c1 + 0xffffffffu) & 0x80000000u));
+            // keys (16 + pos mod 16) << 8 | value: tags 16..31 (0 = empty), values = bytes 1 and
+            // 3 of the dword
+            const uint32_t T = (perm(r1, r0, 0x0c0c0400u) & 0x0f0fu) | 0x1010u;
+            kp[r][j] = perm(T, w, 0x05030401u);
         }
         bend[r] += rdlane(linc, 63);
         bidx[r] += 512u;
@@ -341,17 +353,19 @@ __device__ __forceinline__ void decode_fast(const FastHdr &H, uint8_t *smem, con
         if (bidx[r] >= np[r]) slen[r] = bend[r];
     };
     auto write_keys = [&](int r, uint32_t wstart, uint32_t genk) __attribute__((always_inline)) {
+        const int32_t c = 2 * ((int32_t)wstart - P0[r]) - (int32_t)hbase[r];
+        const int32_t lo = (int32_t)hbase[r] - 2, hi = (int32_t)(hbase[r] + 2u * wlen[r]);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const uint32_t k = kp[r][j] | genk;
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
-                const uint32_t rel = st[r][2 * j + h] - wstart;
-                const uint32_t slot = rel < wlen[r] ? rel : wlen[r];
+                const int32_t v = (int32_t)((uint32_t)st[r][2 * j + h] - (uint32_t)c);
+                const int32_t a = med3_i32(v, lo, hi);  // (lo, hi: VGPR copies, per window)
 #ifndef PSY_X_NOKEYS
-                *reinterpret_cast<uint16_t *>(smem + hbase[r] + 2u * slot) = (uint16_t)(h ? (k >> 16) : k);
+                *reinterpret_cast<uint16_t *>(smem + a) = (uint16_t)(h ? (k >> 16) : k);
 #else
-                if (slot == 0xfffffu) *reinterpret_cast<uint16_t *>(smem + hbase[r]) = (uint16_t)k;
+                if (a == 0xfffff) *reinterpret_cast<uint16_t *>(smem + hbase[r]) = (uint16_t)k;
 #endif
             }
         }
@@ -372,21 +386,34 @@ __device__ __forceinline__ void decode_fast(const FastHdr &H, uint8_t *smem, con
             }
             bidx[r] = 512u * b;
             bend[r] = sp;
-            load_block(r);
-            // the carry: the value at position P - 1, i.e. of the valid pair with the largest
-            // start <= P - 1 (it lies in this block)
-            uint32_t best = 0, bv = 0;
+            {
+                // the carry: the value at position P - 1, i.e. of the last pair with a count that
+                // starts at or before P - 1 (it lies in block b; starts of counted pairs increase)
+                const uint32_t p0 = bidx[r] + 8u * lane;
+                const uint32_t nv = p0 < np[r] ? (np[r] - p0 < 8u ? np[r] - p0 : 8u) : 0u;
+                const uint4 pv =
+                    nv ? ld16_span(blob + soff[r] + 2ull * p0, (int)(2 * nv), blim) : make_uint4(0, 0, 0, 0);
+                const uint32_t pw[4] = {pv.x, pv.y, pv.z, pv.w};
+                uint32_t tot = 0;
 #pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                const uint32_t sti = st[r][i];
-                if (sti != ~0u && sti <= P - 1u && sti + 1u > best) {
-                    best = sti + 1u;
-                    bv = (kp[r][i >> 1] >> (16 * (i & 1))) & 0xffu;
+                for (int j = 0; j < 4; ++j) tot += (pw[j] & 0xffu) + ((pw[j] >> 16) & 0xffu);
+                uint32_t run = sp + wave_incl_scan<OpAdd>(tot) - tot;
+                bool any = false;
+                uint32_t bv = 0;
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const uint32_t w = pw[i >> 1] >> (16 * (i & 1));
+                    const uint32_t cnt = w & 0xffu;
+                    if (cnt != 0u && run <= P - 1u) {
+                        any = true;
+                        bv = (w >> 8) & 0xffu;
+                    }
+                    run += cnt;
                 }
+                const uint64_t who = __ballot(any);
+                cv[r] = who ? rdlane(bv, 63 - (int)__builtin_clzll(who)) : 0u;
             }
-            const uint32_t mx = wave_reduce<OpMax>(best);
-            const uint64_t who = __ballot(best != 0u && best == mx);
-            cv[r] = who ? rdlane(bv, (int)__builtin_ctzll(who)) : 0u;
+            load_block(r);
         }
     }
     const bool dal16 = ((uintptr_t)dst & 15) == 0;
@@ -405,6 +432,14 @@ __device__ __forceinline__ void decode_fast(const FastHdr &H, uint8_t *smem, con
         for (int r = 0; r < 2; ++r) {
             if (r == 1 && !two) break;
             const uint32_t wstart = gwin * seg[r], wend = wstart + wlen[r];
+            if (wstart - (uint32_t)P0[r] >= (1u << PSY_DEC_REBASE_LOG2)) {
+                // rebase the held starts (kept within +-2^30 of the window: the key address
+                // arithmetic is 32-bit; positions per call reach 2^32)
+                const uint32_t d = wstart - (uint32_t)P0[r];
+                P0[r] = (int32_t)wstart;
+#pragma unroll
+                for (int i = 0; i < 8; ++i) st[r][i] = (int32_t)((uint32_t)st[r][i] - 2u * d);
+            }
             if (have[r]) write_keys(r, wstart, genk);
             // blocks whose first pair starts inside this window
             while (bend[r] < wend && bidx[r] < np[r]) {
@@ -439,7 +474,7 @@ __device__ __forceinline__ void decode_fast(const FastHdr &H, uint8_t *smem, con
             // tag (older gens only hold smaller keys); the lane's tag orders the scan, stream-1
             // lanes tagged above every stream-0 lane, so one compare tells a head earlier in the
             // lane's own stream plane from the carry
-            const uint32_t lk = m >= ((gen << 13) | 0x100u) ? perm(ltag, m, 0x07060500u) : 0u;
+            const uint32_t lk = m >= ((gen << 13) | 0x1000u) ? perm(ltag, m, 0x07060500u) : 0u;
             const uint32_t ex = wave_shr1(wave_incl_scan<OpMax>(lk), 0u);
             const uint32_t carry = f1 ? cv[1] : cv[0];
             const uint32_t seedv = ex >= lthr ? (ex & 0xffu) : carry;

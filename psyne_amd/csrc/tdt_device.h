@@ -54,6 +54,14 @@ __device__ __forceinline__ uint32_t dpp_mov(uint32_t x) {
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROWMASK, BANKMASK, false);
 }
 
+// v_med3_i32 (clamp x to [lo, hi] in one VALU; clang folds smax(smin()) into it only for
+// constant bounds)
+__device__ __forceinline__ int32_t med3_i32(int32_t x, int32_t lo, int32_t hi) {
+    int32_t r;
+    asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(lo), "v"(hi));
+    return r;
+}
+
 struct OpAdd {
     __device__ __forceinline__ static uint32_t f(uint32_t a, uint32_t b) { return a + b; }
 };
