@@ -180,6 +180,12 @@ struct tdt_ctx {
         hipEvent_t evi = nullptr;  // after the chunk's input copy (orders the next chunk's)
         PlanWS pw;
     } hs[kHostSlots];
+    // the host pipeline's two streams (chunk buffers stay per slot): every input copy on `hin`, in
+    // chunk order; every kernel and read-back on `hex`.  Per-slot streams (PSYNE_TDT_SLOT_STREAMS=1,
+    // round 4) outnumber the HIP runtime's default 4 hardware queues together with the caller's
+    // streams: streams sharing a queue serialised the chunks (profiles/r05_diag/host_decode/)
+    hipStream_t hin = nullptr, hex = nullptr;
+    bool slot_streams = false;
     // one-message fast path (tdt_encode_host / tdt_decode_host with one message of at most
     // kOneMax bytes: the per-call Protocol::encode / decode of the drop-in class): a mapped pinned
     // block holding the call's offsets, list, status, input and output, read and written by ONE
@@ -209,9 +215,8 @@ struct tdt_ctx {
     bool no_two_phase = false;  // PSYNE_TDT_NO_TWO_PHASE: compacted calls take the one-pass kernels
     bool no_one = false;        // PSYNE_TDT_NO_ONE: one-message host calls take the pipeline too
     bool one_wave = false;      // PSYNE_TDT_ONE_WAVE=1: one-message decode as one wave (round-4 path)
-    uint64_t one_wave_max = 4096;
+    uint64_t one_wave_max = 4096;  // one-message decode: outputs up to this size take the one-wave kernel
     bool dout_sdma = false;     // PSYNE_TDT_DOUT_SDMA=1: host_decode's output by hipMemcpyAsync (round 4)
-    bool h2d_order = true;      // PSYNE_TDT_H2D_ORDER=0: host_decode chunks' input copies unordered (round 4)  // one-message decode: outputs up to this size take the one-wave kernel
     bool one_spin = true;       // PSYNE_TDT_ONE_SPIN=0: one-message calls wait in hipStreamSynchronize
     uint32_t one_seq = 0;
     uint32_t copy_wgs = 8;      // PSYNE_TDT_COPY_WGS: copy-list workgroups per CU
@@ -378,13 +383,36 @@ int ensure_plan(PlanWS &w, uint32_t n, hipStream_t s) {
     return TDT_OK;
 }
 
+// Small device → pinned-host copies (plan counters, a host chunk's lengths / statuses / error
+// flags) as one kernel's stores over PCIe rather than DMA commands: a DMA read-back queued behind
+// a chunk's kernels held up the next chunks' input DMAs behind it (profiles/r05_diag/host_decode/)
+struct SmallCopies {
+    const uint32_t *src[3];
+    uint32_t *dst[3];
+    uint32_t words[3];
+};
+__global__ __launch_bounds__(256) void small_copy_kernel(SmallCopies a) {
+    for (int k = 0; k < 3; ++k)
+        for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < a.words[k]; i += gridDim.x * 256) a.dst[k][i] = a.src[k][i];
+}
+int small_copies(hipStream_t s, const void *s0, void *d0, size_t b0, const void *s1 = nullptr, void *d1 = nullptr,
+                 size_t b1 = 0, const void *s2 = nullptr, void *d2 = nullptr, size_t b2 = 0) {
+    SmallCopies a{{static_cast<const uint32_t *>(s0), static_cast<const uint32_t *>(s1), static_cast<const uint32_t *>(s2)},
+                  {static_cast<uint32_t *>(d0), static_cast<uint32_t *>(d1), static_cast<uint32_t *>(d2)},
+                  {(uint32_t)(b0 / 4), (uint32_t)(b1 / 4), (uint32_t)(b2 / 4)}};
+    const size_t mx = std::max(b0, std::max(b1, b2)) / 4;
+    hipLaunchKernelGGL(small_copy_kernel, dim3((uint32_t)std::min<size_t>(64, mx / 1024 + 1)), dim3(256), 0, s, a);
+    HIPCHK(hipGetLastError());
+    return TDT_OK;
+}
+
 // The plan counters of this call → pinned snapshot (not under stream capture).
 int record_counts(CountHist &h, const void *dcnt, uint32_t n_msgs, hipStream_t s) {
     if (!h.pin) {
         HIPCHK(hipHostMalloc(&h.pin, 128, hipHostMallocDefault));
         HIPCHK(hipEventCreateWithFlags(&h.ev, hipEventDisableTiming));
     }
-    HIPCHK(hipMemcpyAsync(h.pin, dcnt, 128, hipMemcpyDeviceToHost, s));
+    if (int st = small_copies(s, dcnt, h.pin, 128)) return st;
     HIPCHK(hipEventRecord(h.ev, s));
     h.n_pending = n_msgs;
     h.pending = true;
@@ -982,6 +1010,10 @@ bool is_pinned(const void *p) {
 
 int ensure_slot(tdt_ctx *c, int k, size_t dev_bytes, size_t pin_words, size_t sin, size_t sout) {
     auto &h = c->hs[k];
+    if (!c->hin) {
+        HIPCHK(hipStreamCreateWithFlags(&c->hin, hipStreamNonBlocking));
+        HIPCHK(hipStreamCreateWithFlags(&c->hex, hipStreamNonBlocking));
+    }
     if (!h.stream) {
         h.pw.no_side = true;
         HIPCHK(hipStreamCreateWithFlags(&h.stream, hipStreamNonBlocking));
@@ -1028,8 +1060,18 @@ int ensure_slot(tdt_ctx *c, int k, size_t dev_bytes, size_t pin_words, size_t si
 }
 
 // After a slot's stream has drained: fold its last chunk's device error flags into the context.
+// every host-pipeline stream idle (an error mid-pipeline: copies and kernels may still touch the
+// caller's buffers)
+void drain_host(tdt_ctx *c) {
+    for (auto &h : c->hs)
+        if (h.stream) (void)hipStreamSynchronize(h.stream);
+    if (c->hin) (void)hipStreamSynchronize(c->hin);
+    if (c->hex) (void)hipStreamSynchronize(c->hex);
+}
+
 int sync_slot(tdt_ctx *c, tdt_ctx::HostSlot &h) {
-    HIPCHK(hipStreamSynchronize(h.stream));
+    // (the slot's last command is its chunk's h.ev record; never recorded: complete)
+    HIPCHK(c->slot_streams ? hipStreamSynchronize(h.stream) : hipEventSynchronize(h.ev));
     if (h.flag) {
         c->host_flags.fetch_or(*h.flag);
         *h.flag = 0;
@@ -1319,52 +1361,57 @@ int host_encode(tdt_ctx *c, const uint8_t *h_in, const uint64_t *h_in_off, uint3
         auto *dooff = reinterpret_cast<uint64_t *>(d + k.o_ooff);
         auto *dst = reinterpret_cast<int32_t *>(d + k.o_st);
         auto *dlen = reinterpret_cast<uint64_t *>(d + k.o_len);
+        const hipStream_t s_in = c->slot_streams ? h.stream : c->hin, s_ex = c->slot_streams ? h.stream : c->hex;
         if (src) {
-            HIPCHK(hipMemcpyAsync(d, src, k.in_bytes, hipMemcpyHostToDevice, h.stream));
+            HIPCHK(hipMemcpyAsync(d, src, k.in_bytes, hipMemcpyHostToDevice, s_in));
         } else {
             for (uint32_t i = 0; i < k.n;) {
                 const uint8_t *p0 = msgs[k.m0 + i];
                 uint64_t len = sizes[k.m0 + i];
                 uint32_t j = i + 1;
                 while (j < k.n && msgs[k.m0 + j] == p0 + len) len += sizes[k.m0 + j++];
-                if (len) HIPCHK(hipMemcpyAsync(d + pin_in_off[i], p0, len, hipMemcpyHostToDevice, h.stream));
+                if (len) HIPCHK(hipMemcpyAsync(d + pin_in_off[i], p0, len, hipMemcpyHostToDevice, s_in));
                 i = j;
             }
         }
         // in_off and (slotted) the slots: one copy
-        HIPCHK(hipMemcpyAsync(doff, pin_in_off, (k.scap ? 16ull : 8ull) * (k.n + 1), hipMemcpyHostToDevice, h.stream));
+        HIPCHK(hipMemcpyAsync(doff, pin_in_off, (k.scap ? 16ull : 8ull) * (k.n + 1), hipMemcpyHostToDevice, s_in));
+        if (s_in != s_ex) {
+            HIPCHK(hipEventRecord(h.evi, s_in));
+            HIPCHK(hipStreamWaitEvent(s_ex, h.evi, 0));
+        }
         if (k.scap) {
             st = encode_common(c, psy::MODE_ENCODE, d, doff, k.n, nullptr, d + k.o_sbuf, k.scap, nullptr, dst, nullptr,
-                               nullptr, nullptr, h.stream, dslot, dlen, d + k.o_ws, &h.pw);
+                               nullptr, nullptr, s_ex, dslot, dlen, d + k.o_ws, &h.pw);
             if (st) return st;
-            hipLaunchKernelGGL(host_scan_kernel, dim3(1), dim3(1024), 0, h.stream, dlen, dooff, k.n);
+            hipLaunchKernelGGL(host_scan_kernel, dim3(1), dim3(1024), 0, s_ex, dlen, dooff, k.n);
             HIPCHK(hipGetLastError());
         } else {
             st = encode_common(c, psy::MODE_ENCODE, d, doff, k.n, nullptr, d + k.o_out, k.cap, dooff, dst, nullptr,
-                               nullptr, nullptr, h.stream, nullptr, nullptr, d + k.o_ws, nullptr,
+                               nullptr, nullptr, s_ex, nullptr, nullptr, d + k.o_ws, nullptr,
                                k.in_bytes <= kSmallMax * k.n ? 1 : 0);  // (the chunk's sizes are host data)
             if (st) return st;
         }
         // the output, in chunk order (each copy follows the previous chunk's: the running base)
-        if (ci == 0) HIPCHK(hipMemsetAsync(c->hbases, 0, 8, h.stream));
-        else HIPCHK(hipStreamWaitEvent(h.stream, c->hs[(ci - 1) % kHostSlots].evc, 0));
+        if (ci == 0) HIPCHK(hipMemsetAsync(c->hbases, 0, 8, s_ex));
+        else if (c->slot_streams) HIPCHK(hipStreamWaitEvent(s_ex, c->hs[(ci - 1) % kHostSlots].evc, 0));
         uint8_t *odst = pin_out ? d_out : h.stage_out;
         if (k.scap) {
             const uint32_t P = (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(1, k.in_bytes / k.n / 16384));
             const uint32_t grid = (uint32_t)std::min<uint64_t>(2048, ((uint64_t)k.n * P + 3) / 4);
-            hipLaunchKernelGGL(host_gather_kernel, dim3(grid), dim3(256), 0, h.stream, d + k.o_sbuf, dslot, dlen, dooff,
+            hipLaunchKernelGGL(host_gather_kernel, dim3(grid), dim3(256), 0, s_ex, d + k.o_sbuf, dslot, dlen, dooff,
                                k.n, P, odst, c->hbases, (uint32_t)ci, out_cap, pin_out ? 1 : 0);
         } else {
             const uint32_t grid = (uint32_t)std::min<uint64_t>(1024, k.cap / 4096 + 1);
-            hipLaunchKernelGGL(host_out_kernel, dim3(grid), dim3(256), 0, h.stream, d + k.o_out, dooff, k.n, odst,
+            hipLaunchKernelGGL(host_out_kernel, dim3(grid), dim3(256), 0, s_ex, d + k.o_out, dooff, k.n, odst,
                                c->hbases, (uint32_t)ci, out_cap, pin_out ? 1 : 0);
         }
         HIPCHK(hipGetLastError());
-        HIPCHK(hipEventRecord(h.evc, h.stream));
-        HIPCHK(hipMemcpyAsync(h.flag, d + k.o_ws + 4, 4, hipMemcpyDeviceToHost, h.stream));
-        HIPCHK(hipMemcpyAsync(pin_back(h, k), dooff, 8ull * (k.n + 1), hipMemcpyDeviceToHost, h.stream));
-        HIPCHK(hipMemcpyAsync(pin_status(h, k), dst, 4ull * k.n, hipMemcpyDeviceToHost, h.stream));
-        HIPCHK(hipEventRecord(h.ev, h.stream));
+        if (c->slot_streams) HIPCHK(hipEventRecord(h.evc, s_ex));
+        if ((st = small_copies(s_ex, d + k.o_ws + 4, h.flag, 4, dooff, pin_back(h, k), 8ull * (k.n + 1), dst,
+                               pin_status(h, k), 4ull * k.n)))
+            return st;
+        HIPCHK(hipEventRecord(h.ev, s_ex));
         return TDT_OK;
     };
     // chunk ci's compacted size is known once its event fires; then its output comes back
@@ -1451,27 +1498,29 @@ int host_decode(tdt_ctx *c, const uint8_t *h_in, const uint64_t *h_in_off, uint3
         // several slots share the link and all land late, the earliest-needed one included
         // (decode 31 -> 37 GiB/s pinned; the same ordering cost host_encode 44 -> 36 GiB/s,
         // profiles/r05_diag/host_decode/)
-        if (ci > 0 && c->h2d_order) HIPCHK(hipStreamWaitEvent(h.stream, c->hs[(ci - 1) % kHostSlots].evi, 0));
-        HIPCHK(hipMemcpyAsync(d, src, k.in_bytes, hipMemcpyHostToDevice, h.stream));
-        HIPCHK(hipEventRecord(h.evi, h.stream));
-        HIPCHK(hipMemcpyAsync(doff, pin_in_off, 16ull * (k.n + 1), hipMemcpyHostToDevice, h.stream));  // offsets + slots
-        st = decode_common(c, false, d, doff, k.n, d + k.o_out, 0, nullptr, nullptr, dst, h.stream, dslot, dlen,
+        const hipStream_t s_in = c->slot_streams ? h.stream : c->hin, s_ex = c->slot_streams ? h.stream : c->hex;
+        if (ci > 0 && c->slot_streams) HIPCHK(hipStreamWaitEvent(s_in, c->hs[(ci - 1) % kHostSlots].evi, 0));
+        HIPCHK(hipMemcpyAsync(d, src, k.in_bytes, hipMemcpyHostToDevice, s_in));
+        HIPCHK(hipMemcpyAsync(doff, pin_in_off, 16ull * (k.n + 1), hipMemcpyHostToDevice, s_in));  // offsets + slots
+        HIPCHK(hipEventRecord(h.evi, s_in));
+        if (s_in != s_ex) HIPCHK(hipStreamWaitEvent(s_ex, h.evi, 0));
+        st = decode_common(c, false, d, doff, k.n, d + k.o_out, 0, nullptr, nullptr, dst, s_ex, dslot, dlen,
                            nullptr, d + k.o_ws, &h.pw);
         if (st) return st;
-        HIPCHK(hipMemcpyAsync(h.flag, d + k.o_ws + 4, 4, hipMemcpyDeviceToHost, h.stream));
         if (acc && dma_out) {
             HIPCHK(hipMemcpyAsync(pin_out ? h_out + k.base : h.stage_out, d + k.o_out, acc, hipMemcpyDeviceToHost,
-                                  h.stream));
+                                  s_ex));
         } else if (acc) {
             // the output crosses PCIe as a copy kernel's stores (as host_encode's), not a DMA: the
             // DMA engines then carry only the H2D direction
             hipLaunchKernelGGL(host_dout_kernel, dim3((uint32_t)std::min<uint64_t>(1024, acc / 4096 + 1)), dim3(256), 0,
-                               h.stream, d + k.o_out, pin_out ? d_hout + k.base : h.stage_out, acc);
+                               s_ex, d + k.o_out, pin_out ? d_hout + k.base : h.stage_out, acc);
             HIPCHK(hipGetLastError());
         }
-        HIPCHK(hipMemcpyAsync(pin_back(h, k), dlen, 8ull * k.n, hipMemcpyDeviceToHost, h.stream));
-        HIPCHK(hipMemcpyAsync(pin_status(h, k), dst, 4ull * k.n, hipMemcpyDeviceToHost, h.stream));
-        HIPCHK(hipEventRecord(h.ev, h.stream));
+        if ((st = small_copies(s_ex, d + k.o_ws + 4, h.flag, 4, dlen, pin_back(h, k), 8ull * k.n, dst,
+                               pin_status(h, k), 4ull * k.n)))
+            return st;
+        HIPCHK(hipEventRecord(h.ev, s_ex));
         return TDT_OK;
     };
     auto finish = [&](size_t ci) -> int {
@@ -1678,8 +1727,7 @@ int host_path(tdt_ctx *c, bool encode, const uint8_t *h_in, const uint64_t *h_in
     if (st != TDT_OK) {
         // an error mid-pipeline: the other slot's copies and kernels may still read the caller's
         // input or write its output — drain both slots before the caller gets its buffers back
-        for (auto &h : c->hs)
-            if (h.stream) (void)hipStreamSynchronize(h.stream);
+        drain_host(c);
         (void)hipGetLastError();
     }
     return st;
@@ -1771,7 +1819,7 @@ int tdt_ctx_create(int device, const tdt_config *cfg, tdt_ctx **out) {
     x->no_one = flag("PSYNE_TDT_NO_ONE");
     x->one_wave = flag("PSYNE_TDT_ONE_WAVE");
     x->dout_sdma = flag("PSYNE_TDT_DOUT_SDMA");
-    if (const char *e = std::getenv("PSYNE_TDT_H2D_ORDER")) x->h2d_order = *e == '1';
+    x->slot_streams = flag("PSYNE_TDT_SLOT_STREAMS");
     if (const char *e = std::getenv("PSYNE_TDT_ONE_SPIN")) x->one_spin = *e == '1';
     if (const char *e = std::getenv("PSYNE_TDT_DBIG_MIN")) x->dbig_min = std::strtoull(e, nullptr, 10);
     if (const char *e = std::getenv("PSYNE_TDT_DSMALL_MAX")) x->dsmall_max = std::strtoull(e, nullptr, 10);
@@ -1819,6 +1867,10 @@ void tdt_ctx_destroy(tdt_ctx *ctx) {
         if (h.evi) (void)hipEventDestroy(h.evi);
         if (h.stream) (void)hipStreamDestroy(h.stream);
     }
+    if (ctx->hin) (void)hipStreamSynchronize(ctx->hin);
+    if (ctx->hex) (void)hipStreamSynchronize(ctx->hex);
+    if (ctx->hin) (void)hipStreamDestroy(ctx->hin);
+    if (ctx->hex) (void)hipStreamDestroy(ctx->hex);
     delete ctx;
 }
 
@@ -2059,8 +2111,7 @@ int tdt_encode_host_v(tdt_ctx *ctx, const uint8_t *const *msgs, const uint64_t *
     if (!ctx->pool) ctx->pool.reset(new CopyPool(ctx->copy_threads));
     const int st = host_encode(ctx, nullptr, voff.data(), n_msgs, h_out, out_cap, h_out_off, h_status, msgs, sizes);
     if (st != TDT_OK) {
-        for (auto &h : ctx->hs)
-            if (h.stream) (void)hipStreamSynchronize(h.stream);
+        drain_host(ctx);
         (void)hipGetLastError();
     }
     return st;
