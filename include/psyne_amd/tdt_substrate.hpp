@@ -24,7 +24,7 @@
 //     (every method here matches its signature, so it overrides), an empty struct otherwise.
 //     send_batch / receive_batch move many messages per GPU call through the C ABI host
 //     pipeline (tdt_encode_host_v / tdt_decode_host: chunked, H2D / kernel / D2H of neighbouring
-//     chunks overlapped over four pipeline slots) with a sender and a receiver thread overlapping
+//     chunks overlapped over four pipeline slots on two streams) with a sender and a receiver thread overlapping
 //     the socket with the codec,
 //     which is how the codec reaches the link's rate instead of per-message latency.
 #pragma once

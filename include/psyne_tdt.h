@@ -164,8 +164,9 @@ int tdt_analyze_batch(tdt_ctx *ctx, const uint8_t *d_in, const uint64_t *d_in_of
                       void *hip_stream);
 
 /* Host-memory path (the TCP socket-buffer case).  The batch runs as chunks (an eighth of the
- * call's input, 2-64 MiB) through four pipeline slots, each its own stream: H2D, kernel and D2H of
- * neighbouring chunks overlap.  Pinned caller buffers are DMA'd
+ * call's input, 2-64 MiB) through four pipeline slots (device buffers) on two streams, one for
+ * the input DMAs and one for the kernels and the output: H2D, kernel and D2H of neighbouring
+ * chunks overlap.  Pinned caller buffers are DMA'd
  * directly; pageable ones (std::vector, numpy) are staged through the context's pinned buffers
  * by a pool of host threads (TDT_OPT_COPY_THREADS).  h_out must hold the sum of
  * tdt_encode_bound (encode) or of the decoded sizes (decode); h_out_off receives n+1 offsets.
