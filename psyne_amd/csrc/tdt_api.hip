@@ -1114,7 +1114,8 @@ Chunk plan_chunk(const uint64_t *h_in_off, uint32_t m0, uint32_t n_msgs, bool en
     k.scap = encode && slotted ? cap : 0;
     k.o_off = align_up(k.in_bytes, 256);
     k.o_out = align_up(k.o_off + 16ull * (k.n + 1), 256);
-    k.o_ooff = align_up(k.o_out + std::max<uint64_t>(cap, 1), 256);
+    // (the slotted encode writes its blobs into the slot buffer at o_sbuf: no compacted region)
+    k.o_ooff = align_up(k.o_out + (k.scap ? 1ull : std::max<uint64_t>(cap, 1)), 256);
     k.o_st = align_up(k.o_ooff + 8ull * (k.n + 1), 256);
     k.o_ws = align_up(k.o_st + 4ull * k.n, 256);
     k.o_len = align_up(k.o_ws + kCounterBytes + 8ull * (k.n + 1), 256);

@@ -292,14 +292,16 @@ __device__ __forceinline__ void decode_fast(const FastHdr &H, uint8_t *smem, con
     const uint32_t fh = (f1 ? hbase[1] : hbase[0]) + 2u * fu;
     const uint32_t last_lane0 = 4u * seg[0] - 1u;  // lane holding stream 0's last plane byte
     // recombine: S dword d (S = the group's seg[0] stream-0 bytes, then its seg[1] stream-1
-    // bytes) = plane bytes sd_pb[d] + lane·sd_mul[d] (4 bytes of one stream: seg[r] % 4 == 0)
-    uint32_t sd_pb[4], sd_mul[4];
+    // bytes) = plane bytes sd_pb[d] + lane·sd_mul[d] (4 bytes of one stream: seg[r] % 4 == 0),
+    // held per lane (sd_off: VGPRs, so the round loop needs no SGPRs for them)
+    uint32_t sd_pb[4], sd_mul[4], sd_off[4];
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
         const uint32_t r = 4u * (uint32_t)d >= seg[0] ? 1u : 0u;
         const uint32_t u = 4u * (uint32_t)d - (r ? seg[0] : 0u);
         sd_pb[d] = (r ? 64u * seg[0] : 0u) + u;
         sd_mul[d] = r ? seg[1] : seg[0];
+        sd_off[d] = sd_pb[d] + lane * sd_mul[d];
     }
 
     // per stream block state (uniform) and registers (per lane)
@@ -417,6 +419,9 @@ __device__ __forceinline__ void decode_fast(const FastHdr &H, uint8_t *smem, con
         }
     }
     const bool dal16 = ((uintptr_t)dst & 15) == 0;
+    // whole 16-byte groups of the output (a 32-bit uniform compare per round: gfx9 has no scalar
+    // u64 less-than)
+    const uint32_t wg16 = (uint32_t)(wbytes >> 4);
     uint32_t win = 0;
     for (uint32_t gwin = g_lo; gwin < g_hi; gwin += 64u * WR, ++win) {
         const uint32_t gen = win & 7u;
@@ -513,14 +518,14 @@ __device__ __forceinline__ void decode_fast(const FastHdr &H, uint8_t *smem, con
             } else {
 #pragma unroll
                 for (int d = 0; d < 4; ++d)
-                    S[d] = *reinterpret_cast<const uint32_t *>(planes + sd_pb[d] + lane * sd_mul[d]);
+                    S[d] = *reinterpret_cast<const uint32_t *>(planes + sd_off[d]);
             }
             const uint4 o = make_uint4(perm(S[1], S[0], OA[0]) | perm(S[3], S[2], OB[0]),
                                        perm(S[1], S[0], OA[1]) | perm(S[3], S[2], OB[1]),
                                        perm(S[1], S[0], OA[2]) | perm(S[3], S[2], OB[2]),
                                        perm(S[1], S[0], OA[3]) | perm(S[3], S[2], OB[3]));
             const uint32_t g = g0 + lane;
-            if (dal16 && 16ull * (g0 + 64u) <= wbytes) {
+            if (dal16 && g0 + 64u <= wg16) {
                 // a whole aligned round (uniform): one 16-byte store per lane, no per-lane tests
 #ifndef PSY_X_NOSTORE
                 st16_nt(dst + 16ull * g, o);
