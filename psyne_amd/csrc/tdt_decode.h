@@ -327,27 +327,70 @@ __device__ __forceinline__ void decode_fast(const FastHdr &H, uint8_t *smem, con
 
     auto load_block = [&](int r) __attribute__((always_inline)) {
         const uint32_t p0 = bidx[r] + 8u * lane;
-        const uint32_t nv = p0 < np[r] ? (np[r] - p0 < 8u ? np[r] - p0 : 8u) : 0u;
-        const uint4 pv = nv ? ld16_span(blob + soff[r] + 2ull * p0, (int)(2 * nv), blim) : make_uint4(0, 0, 0, 0);
+        // (uniform) a block before the stream's last: every lane holds 8 pairs, read with plain
+        // aligned dword loads (the dword after them, read when the pairs are not dword-aligned,
+        // holds a byte of the next pair: no bounds tests) — else the checked, zero-filled load
+        const bool full = bidx[r] + 512u < np[r];
+        uint4 pv;
+        if (full) {
+            const uint8_t *sb = blob + soff[r];
+            const uint32_t sh = (uint32_t)__builtin_amdgcn_readfirstlane((int)((uintptr_t)sb & 3u));
+            const uint32_t *q = reinterpret_cast<const uint32_t *>(((uintptr_t)sb & ~(uintptr_t)3) + 2ull * p0);
+            const uint32_t w0 = gload<uint32_t>(q), w1 = gload<uint32_t>(q + 1), w2 = gload<uint32_t>(q + 2),
+                           w3 = gload<uint32_t>(q + 3);
+            if (sh == 0u) {
+                pv = make_uint4(w0, w1, w2, w3);
+            } else {
+                const uint32_t w4 = gload<uint32_t>(q + 4);
+                pv = make_uint4(__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
+                                __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh));
+            }
+        } else {
+            const uint32_t nv = p0 < np[r] ? (np[r] - p0 < 8u ? np[r] - p0 : 8u) : 0u;
+            pv = nv ? ld16_span(blob + soff[r] + 2ull * p0, (int)(2 * nv), blim) : make_uint4(0, 0, 0, 0);
+        }
         const uint32_t pw[4] = {pv.x, pv.y, pv.z, pv.w};
-        const uint32_t s2 = (pw[0] & 0x00ff00ffu) + (pw[1] & 0x00ff00ffu) + (pw[2] & 0x00ff00ffu) + (pw[3] & 0x00ff00ffu);
+        const uint32_t cw[4] = {pw[0] & 0x00ff00ffu, pw[1] & 0x00ff00ffu, pw[2] & 0x00ff00ffu, pw[3] & 0x00ff00ffu};
+        const uint32_t s2 = cw[0] + cw[1] + cw[2] + cw[3];
         const uint32_t tot = (s2 & 0xffffu) + (s2 >> 16);
         const uint32_t linc = wave_incl_scan<OpAdd>(tot);
         // this lane's first start - P0 (P0 % 16 == 0: the low 4 bits are the position mod 16)
         uint32_t run = bend[r] - (uint32_t)P0[r] + linc - tot;
+        // (uniform) a full block whose pairs all carry a count (psyne's encoder writes no count-0
+        // pairs; past a stream's end the zero-filled loads do): starts held without the flag
+        bool counted = false;
+#ifndef PSY_X_NOCOUNTED
+        if (full) {
+            const uint32_t mn = pk_min_u16(pk_min_u16(cw[0], cw[1]), pk_min_u16(cw[2], cw[3]));
+            counted = !__any((mn & 0xffffu) == 0u || (mn >> 16) == 0u);
+        }
+#endif
+        if (counted) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint32_t w = pw[j];
-            const uint32_t c0 = w & 0xffu, c1 = (w >> 16) & 0xffu;
-            const uint32_t r0 = run, r1 = run + c0;
-            run = r1 + c1;
-            // (pairs past the stream's end were loaded as zero bytes: count 0, no extra test)
-            st[r][2 * j] = (int32_t)((r0 << 1) | ((c0 + 0xffffffffu) & 0x80000000u));
-            st[r][2 * j + 1] = (int32_t)((r1 << 1) | ((c1 + 0xffffffffu) & 0x80000000u));
-            // keys (16 + pos mod 16) << 8 | value: tags 16..31 (0 = empty), values = bytes 1 and
-            // 3 of the dword
-            const uint32_t T = (perm(r1, r0, 0x0c0c0400u) & 0x0f0fu) | 0x1010u;
-            kp[r][j] = perm(T, w, 0x05030401u);
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t w = pw[j];
+                const uint32_t r0 = run, r1 = run + (w & 0xffu);
+                run = r1 + ((w >> 16) & 0xffu);
+                st[r][2 * j] = (int32_t)add_self(r0);
+                st[r][2 * j + 1] = (int32_t)add_self(r1);
+                const uint32_t T = (perm(r1, r0, 0x0c0c0400u) & 0x0f0fu) | 0x1010u;
+                kp[r][j] = perm(T, w, 0x05030401u);
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t w = pw[j];
+                const uint32_t c0 = w & 0xffu, c1 = (w >> 16) & 0xffu;
+                const uint32_t r0 = run, r1 = run + c0;
+                run = r1 + c1;
+                // (pairs past the stream's end were loaded as zero bytes: count 0, no extra test)
+                st[r][2 * j] = (int32_t)((r0 << 1) | ((c0 + 0xffffffffu) & 0x80000000u));
+                st[r][2 * j + 1] = (int32_t)((r1 << 1) | ((c1 + 0xffffffffu) & 0x80000000u));
+                // keys (16 + pos mod 16) << 8 | value: tags 16..31 (0 = empty), values = bytes 1
+                // and 3 of the dword
+                const uint32_t T = (perm(r1, r0, 0x0c0c0400u) & 0x0f0fu) | 0x1010u;
+                kp[r][j] = perm(T, w, 0x05030401u);
+            }
         }
         bend[r] += rdlane(linc, 63);
         bidx[r] += 512u;

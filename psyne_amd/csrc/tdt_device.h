@@ -62,6 +62,13 @@ __device__ __forceinline__ int32_t med3_i32(int32_t x, int32_t lo, int32_t hi) {
     return r;
 }
 
+// 2x as v_add_u32 x, x (a fast-issue add; clang turns x + x into v_lshlrev_b32, a slow one)
+__device__ __forceinline__ uint32_t add_self(uint32_t x) {
+    uint32_t r;
+    asm("v_add_u32 %0, %1, %1" : "=v"(r) : "v"(x));
+    return r;
+}
+
 struct OpAdd {
     __device__ __forceinline__ static uint32_t f(uint32_t a, uint32_t b) { return a + b; }
 };
@@ -121,6 +128,10 @@ __device__ __forceinline__ uint32_t wave_shl1(uint32_t x, uint32_t old) {
 typedef unsigned short psy_u16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t pk_max_u16(uint32_t a, uint32_t b) {
     return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(psy_u16x2, a),
+                                                                  __builtin_bit_cast(psy_u16x2, b)));
+}
+__device__ __forceinline__ uint32_t pk_min_u16(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(psy_u16x2, a),
                                                                   __builtin_bit_cast(psy_u16x2, b)));
 }
 // (lo, max(hi, lo)) and (max(a.lo, b.hi), max(a.hi, b.hi)): one v_pk_max_u16 each, the half
