@@ -5,7 +5,7 @@ TAG=${1:-run}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-timeout -k 10 300 python -u bench.py --host-inclusive --cpu-seconds 0 --steps 3 --warmup 1 > "$OUT/bench_host.log" 2>&1
+timeout -k 10 300 python -u bench.py --host-inclusive --latency --cpu-seconds 0 --steps 3 --warmup 1 > "$OUT/bench_host.log" 2>&1
 rc=$?; tail -1 "$OUT/bench_host.log"; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 120 ./tests/native/tcp_loopback --codec none --count 1000 --port 18090 > "$OUT/loopback_none.json" 2> "$OUT/loopback_none.err"
 rc=$?; cat "$OUT/loopback_none.json"; [ $rc -eq 0 ] || exit $rc
