@@ -257,15 +257,17 @@ def lib_sha256() -> str:
     return hashlib.sha256(p.read_bytes()).hexdigest()
 
 
-def load_traffic(config_key, sha):
+def load_traffic(config_key, sha, src=None):
     """HBM bytes per launch measured with rocprofv3 PMC passes of THIS library build
-    (profiles/**/*traffic.json with a matching lib_sha256), or None."""
+    (profiles/**/*traffic.json with a matching lib_sha256, or — hipcc builds are not
+    byte-reproducible — with a matching src_sha256: the same kernel sources and build recipe),
+    or None."""
     for p in sorted((ROOT / "profiles").glob("**/*traffic.json")):
         try:
             d = json.loads(p.read_text())
         except Exception:
             continue
-        if d.get("config") == config_key and d.get("lib_sha256") == sha:
+        if d.get("config") == config_key and (d.get("lib_sha256") == sha or (src and d.get("src_sha256") == src)):
             d["_file"] = str(p.relative_to(ROOT))
             return d
     return None
@@ -738,7 +740,9 @@ def main():
         combined = 2 * alg / ((t_enc + t_dec) * 1e-3) / 1e9
         key = "%s_%dx%d" % (a.workload, n, mb)
         sha = lib_sha256()
-        tr = load_traffic(key, sha)
+        from psyne_amd.srchash import src_sha256
+        src = None if os.environ.get("PSYNE_TDT_LIB") else src_sha256()  # (a variant build: its own sha only)
+        tr = load_traffic(key, sha, src)
         traffic = tr["kernels"][dom].get("hbm_bytes_per_launch") if tr and dom in tr.get("kernels", {}) else None
         ceil = copy_ceiling(torch, dev)  # (after the timed region; rank 0)
         cpu = None
@@ -794,6 +798,7 @@ def main():
             "kernels_ms": {"encode": round(t_enc, 4), "decode": round(t_dec, 4)},
             "slots_ms": {"encode_slots": round(t_eslot, 4), "decode_slots": round(t_dslot, 4)},
             "lib_sha256": sha[:16],
+            "src_sha256": src[:16] if src else None,
             "compression_ratio": round(payload / enc_bytes, 4) if enc_bytes else None,
             "roundtrip_ok": ok,
             "per_rank": per_rank,
