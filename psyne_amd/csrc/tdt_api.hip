@@ -1059,7 +1059,6 @@ int ensure_slot(tdt_ctx *c, int k, size_t dev_bytes, size_t pin_words, size_t si
     return TDT_OK;
 }
 
-// After a slot's stream has drained: fold its last chunk's device error flags into the context.
 // every host-pipeline stream idle (an error mid-pipeline: copies and kernels may still touch the
 // caller's buffers)
 void drain_host(tdt_ctx *c) {
@@ -1069,6 +1068,7 @@ void drain_host(tdt_ctx *c) {
     if (c->hex) (void)hipStreamSynchronize(c->hex);
 }
 
+// Once a slot's last chunk is done: fold its device error flags into the context.
 int sync_slot(tdt_ctx *c, tdt_ctx::HostSlot &h) {
     // (the slot's last command is its chunk's h.ev record; never recorded: complete)
     HIPCHK(c->slot_streams ? hipStreamSynchronize(h.stream) : hipEventSynchronize(h.ev));
