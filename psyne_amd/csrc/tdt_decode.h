@@ -251,6 +251,7 @@ struct FastHdr {
     uint32_t orig, ws, two;
     uint32_t seg[2], np[2], soff[2];
     uint32_t OA[4], OB[4];
+    uint32_t rkind;  // recombine form (RecLayout::rkind); OA / OB then hold its selectors
     uint64_t osize;
 };
 
@@ -275,6 +276,7 @@ __device__ __forceinline__ void decode_fast(const FastHdr &H, uint8_t *smem, con
     const uint32_t soff[2] = {U(H.soff[0]), two ? U(H.soff[1]) : 0u};
     const uint32_t OA[4] = {U(H.OA[0]), U(H.OA[1]), U(H.OA[2]), U(H.OA[3])};
     const uint32_t OB[4] = {U(H.OB[0]), U(H.OB[1]), U(H.OB[2]), U(H.OB[3])};
+    const uint32_t rkind = U(H.rkind);
     const uint32_t wlen[2] = {WR * 64u * seg[0], WR * 64u * seg[1]};
     const uint32_t hbase[2] = {(uint32_t)Lay::OFF_FHEADS, (uint32_t)Lay::OFF_FHEADS + 2u * (wlen[0] + 16u)};
     // round rl's plane bytes go to the heads of round rl of the stream with the larger segment
@@ -563,10 +565,24 @@ __device__ __forceinline__ void decode_fast(const FastHdr &H, uint8_t *smem, con
                 for (int d = 0; d < 4; ++d)
                     S[d] = *reinterpret_cast<const uint32_t *>(planes + sd_off[d]);
             }
-            const uint4 o = make_uint4(perm(S[1], S[0], OA[0]) | perm(S[3], S[2], OB[0]),
-                                       perm(S[1], S[0], OA[1]) | perm(S[3], S[2], OB[1]),
-                                       perm(S[1], S[0], OA[2]) | perm(S[3], S[2], OB[2]),
-                                       perm(S[1], S[0], OA[3]) | perm(S[3], S[2], OB[3]));
+            uint4 o;
+            if (rkind == 1u) {
+                o = make_uint4(perm(S[3], S[0], OA[0]), perm(S[3], perm(S[1], S[0], OB[1]), OA[1]),
+                               perm(S[3], perm(S[2], S[1], OB[2]), OA[2]), perm(S[3], S[2], OA[3]));
+            } else if (rkind == 3u) {
+                o = make_uint4(perm(S[2], S[0], OA[0]), perm(S[2], S[0], OA[1]), perm(S[3], S[1], OA[2]),
+                               perm(S[3], S[1], OA[3]));
+            } else if (rkind == 2u) {
+                o = make_uint4(perm(S[0], S[1], OA[0]), perm(S[0], perm(S[2], S[1], OB[1]), OA[1]),
+                               perm(S[0], perm(S[3], S[2], OB[2]), OA[2]), perm(S[0], S[3], OA[3]));
+            } else if (rkind == 4u) {
+                o = make_uint4(S[0], S[1], S[2], S[3]);
+            } else {
+                o = make_uint4(perm(S[1], S[0], OA[0]) | perm(S[3], S[2], OB[0]),
+                               perm(S[1], S[0], OA[1]) | perm(S[3], S[2], OB[1]),
+                               perm(S[1], S[0], OA[2]) | perm(S[3], S[2], OB[2]),
+                               perm(S[1], S[0], OA[3]) | perm(S[3], S[2], OB[3]));
+            }
             const uint32_t g = g0 + lane;
             if (dal16 && g0 + 64u <= wg16) {
                 // a whole aligned round (uniform): one 16-byte store per lane, no per-lane tests
@@ -594,8 +610,13 @@ __device__ __forceinline__ void decode_fast(const FastHdr &H, uint8_t *smem, con
 // r = 0, then its seg[1] bytes of stream r = 1) into word order (recombine :614-637): output
 // byte i = word i / ws, position b = i % ws → S byte (r_b ? seg0 : 0) + (i / ws)·k_b + rank_b.
 // Compiled into constant tables (parse_fast's general derivation handles everything else).
+// Word size 4 has four S-dword structures with cheaper forms than 2 v_perm + v_or per output
+// dword (rkind; OA / OB then hold their selectors): 1 — segments 12 + 4: words 0 and 3 one v_perm
+// of two S dwords, words 1 and 2 two chained v_perm (S0|S1 or S1|S2, then S3); 2 — segments
+// 4 + 12: the same with S0 as the shared dword; 3 — segments 8 + 8: one v_perm per word; 4 — one
+// stream: the S dwords are the words.  0: the general form.
 struct RecLayout {
-    uint32_t two, m0, seg0, seg1, OA[4], OB[4];
+    uint32_t two, m0, seg0, seg1, OA[4], OB[4], rkind;
 };
 template <int WS>
 struct RecTable {
@@ -625,6 +646,75 @@ constexpr RecLayout make_rec_layout(uint32_t mb) {
     for (int q = 0; q < 4; ++q) {
         L.OA[q] = A[q];
         L.OB[q] = B[q];
+    }
+    L.rkind = 0;
+    if (WS == 4) {
+        uint32_t sx[16];  // S byte of output byte i
+        for (uint32_t i = 0; i < 16; ++i) {
+            const uint32_t b = i % WS, v = (mb >> b) & 1u;
+            uint32_t rank = 0;
+            for (uint32_t bb = 0; bb < b; ++bb) rank += ((mb >> bb) & 1u) == v ? 1u : 0u;
+            sx[i] = (v == m0 ? 0u : L.seg0) + (i / WS) * k[v] + rank;
+        }
+        // selector byte j of word q from the S byte s: `lo` = the low operand's first S byte,
+        // `hi` = the high operand's (0x0c: a zero byte)
+        bool ok = true;  // every output byte has a source in its form (else the general form)
+        auto sel = [&](uint32_t q, uint32_t lo, uint32_t hi, uint32_t lo_n, bool partial = false) -> uint32_t {
+            uint32_t r = 0;
+            for (uint32_t j = 0; j < 4; ++j) {
+                const uint32_t x = sx[4 * q + j];
+                uint32_t t = 0x0c;
+                if (x >= lo && x < lo + lo_n) t = x - lo;
+                else if (x >= hi && x < hi + 4) t = 4 + (x - hi);
+                else if (!partial) ok = false;
+                r |= t << (8 * j);
+            }
+            return r;
+        };
+        // chained second step: bytes of the first step's result (t: bytes lo..lo+7) pass as j,
+        // the rest come from the shared dword at `hi`
+        auto sel2 = [&](uint32_t q, uint32_t lo, uint32_t hi) -> uint32_t {
+            uint32_t r = 0;
+            for (uint32_t j = 0; j < 4; ++j) {
+                const uint32_t x = sx[4 * q + j];
+                const bool inl = x >= lo && x < lo + 8;
+                if (!inl && !(x >= hi && x < hi + 4)) ok = false;
+                r |= (inl ? j : 4 + (x - hi)) << (8 * j);
+            }
+            return r;
+        };
+        uint32_t sA[4] = {L.OA[0], L.OA[1], L.OA[2], L.OA[3]}, sB[4] = {L.OB[0], L.OB[1], L.OB[2], L.OB[3]};
+        uint32_t rk = 0;
+        if (L.seg0 == 12 && L.seg1 == 4) {
+            rk = 1;  // o0 = perm(S3, S0), o1 = perm(S3, perm(S1, S0)), o2 = perm(S3, perm(S2, S1)), o3 = perm(S3, S2)
+            sA[0] = sel(0, 0, 12, 4);
+            sB[1] = sel(1, 0, 99, 8, true);
+            sA[1] = sel2(1, 0, 12);
+            sB[2] = sel(2, 4, 99, 8, true);
+            sA[2] = sel2(2, 4, 12);
+            sA[3] = sel(3, 8, 12, 4);
+        } else if (L.seg0 == 4 && L.seg1 == 12) {
+            rk = 2;  // o0 = perm(S0, S1), o1 = perm(S0, perm(S2, S1)), o2 = perm(S0, perm(S3, S2)), o3 = perm(S0, S3)
+            sA[0] = sel(0, 4, 0, 4);
+            sB[1] = sel(1, 4, 99, 8, true);
+            sA[1] = sel2(1, 4, 0);
+            sB[2] = sel(2, 8, 99, 8, true);
+            sA[2] = sel2(2, 8, 0);
+            sA[3] = sel(3, 12, 0, 4);
+        } else if (L.seg0 == 8 && L.seg1 == 8) {
+            rk = 3;  // o_q = perm(S[2 + q/2], S[q/2])
+            for (uint32_t q = 0; q < 4; ++q) sA[q] = sel(q, 4 * (q >> 1), 8 + 4 * (q >> 1), 4);
+        } else if (L.seg0 == 16) {
+            rk = 4;  // one stream: o_q = S_q
+            for (uint32_t i = 0; i < 16; ++i) ok = ok && sx[i] == i;
+        }
+        if (rk && ok) {
+            L.rkind = rk;
+            for (int q = 0; q < 4; ++q) {
+                L.OA[q] = sA[q];
+                L.OB[q] = sB[q];
+            }
+        }
     }
     return L;
 }
@@ -693,6 +783,7 @@ __device__ __forceinline__ FastHdr parse_fast(const uint8_t *blob, uint64_t len,
             h.OA[q] = R.OA[q];
             h.OB[q] = R.OB[q];
         }
+        h.rkind = R.rkind;
         h.orig = orig;
         h.ws = ws;
         h.two = R.two;
