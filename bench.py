@@ -740,8 +740,10 @@ def main():
         combined = 2 * alg / ((t_enc + t_dec) * 1e-3) / 1e9
         key = "%s_%dx%d" % (a.workload, n, mb)
         sha = lib_sha256()
-        from psyne_amd.srchash import src_sha256
-        src = None if os.environ.get("PSYNE_TDT_LIB") else src_sha256()  # (a variant build: its own sha only)
+        from psyne_amd import _lib
+        from psyne_amd.srchash import recorded
+        # the source hash the build recorded beside the library (a variant without one: its sha only)
+        src = recorded(pathlib.Path(os.environ.get("PSYNE_TDT_LIB") or _lib.LIB_PATH))
         tr = load_traffic(key, sha, src)
         traffic = tr["kernels"][dom].get("hbm_bytes_per_launch") if tr and dom in tr.get("kernels", {}) else None
         ceil = copy_ceiling(torch, dev)  # (after the timed region; rank 0)

@@ -506,6 +506,9 @@ public:
         std::lock_guard<std::mutex> a(tx_mu_), b(rx_mu_);
         return st_;
     }
+    // Test hook: the receive pipeline's decoder thread fails on its next buffer, as a failed GPU
+    // decode call does (tests/cpp/test_substrate.cpp: the error must reach the caller).
+    void fail_next_decode_for_test() { fail_decoder_.store(true); }
 
     // Many messages per GPU call: the batch is encoded in sub-batches and queued for the sender
     // thread (one frame per blob, in order).  Returns the wire bytes of this batch.
@@ -734,7 +737,7 @@ private:
     static constexpr size_t kRxFrames = 16384;
     static constexpr size_t kRxMax = 16;  // receive buffers at most (32 MiB of frames each)
     static constexpr uint64_t kRxEager = 4ull << 20;  // an idle decoder gets a buffer once it holds this much
-    static constexpr size_t kMaxFrame = 100ull * 1024 * 1024 + 64;  // the reference's frame cap (tcp_simple.hpp:127-134)
+    static constexpr size_t kMaxFrame = 100ull * 1024 * 1024;  // the reference's frame cap (tcp_simple.hpp:127-134)
 
     using Clock = std::chrono::steady_clock;
     static double since(Clock::time_point t) { return std::chrono::duration<double>(Clock::now() - t).count(); }
@@ -834,10 +837,12 @@ private:
         RxBuf *b = rx_order_.front();
         return b->decoded && b->used < b->n ? b : nullptr;
     }
-    // nothing decoded or still to decode is waiting (rx_mu_ held)
+    // nothing decoded or still to decode is waiting (rx_mu_ held); once the decoder thread has
+    // failed, a sealed buffer it never decoded counts as drained, so its error reaches the caller
+    // instead of every receive waiting forever for those frames
     bool rx_drained() {
         for (RxBuf *b : rx_order_)
-            if (b->sealed && b->used < b->n) return false;
+            if (b->sealed && b->used < b->n && (b->decoded || !dec_dead_)) return false;
         return true;
     }
     bool frames_ready() {
@@ -972,18 +977,18 @@ private:
                 bool got = false;
                 try {
                     // a frame larger than the current capacity (a later call's larger messages)
-                    // grows the buffers instead of reaching Inner with too small a buffer, which
-                    // drops the connection; frames above the reference's 100 MB cap
-                    // are left to Inner, which refuses them as the reference does
+                    // is received into a buffer grown for it alone instead of reaching Inner with
+                    // too small a buffer, which drops the connection: the filling
+                    // buffer is sealed first if it holds frames, and the pool's capacity for
+                    // later buffers is not raised (one 100 MB frame used to make
+                    // every buffer reserve 200 MB of pinned memory).  Frames above the
+                    // reference's 100 MB cap are left to Inner, which refuses them as the
+                    // reference does
                     if constexpr (requires(Inner &s, size_t &l) { s.peek_frame_length(l); }) {
                         size_t l = 0;
                         if (inner_.peek_frame_length(l) && l > fcap && l <= kMaxFrame) {
-                            {
-                                std::lock_guard<std::mutex> lk(rx_mu_);
-                                rx_frame_cap_ = std::max<size_t>(rx_frame_cap_, l);
-                            }
-                            fcap = l;
-                            if (b->n == 0) b->mem.reserve(std::max<uint64_t>(kRxBytes + fcap, 2 * fcap));
+                            fcap = l;  // (b->n > 0: the capacity test below seals b)
+                            if (b->n == 0) b->mem.reserve(fcap);
                         }
                     }
                     if (b->mem.capacity() - b->off[b->n] >= fcap)
@@ -1082,6 +1087,7 @@ private:
             }
             const auto td = Clock::now();
             try {
+                if (fail_decoder_.exchange(false)) throw std::runtime_error("TDT: GPU batch decode failed: injected");
                 b->claim.resize(b->n);
                 b->st.assign(b->n, TDT_OK);
                 b->doff.assign(b->n + 1, 0);
@@ -1118,6 +1124,7 @@ private:
             } catch (...) {
                 std::lock_guard<std::mutex> lk(rx_mu_);
                 rx_err_ = std::current_exception();
+                dec_dead_ = true;  // (this buffer and every later one stay undecoded: rx_drained)
                 rx_cv_.notify_all();
                 return;
             }
@@ -1158,7 +1165,8 @@ private:
     std::vector<RxBuf *> rx_order_;  // buffers in arrival order (the one being filled last)
     size_t rx_frame_cap_ = 0;
     uint64_t rx_max_msg_ = 0;        // largest max_msg of a receive_batch call: the decoder's limit
-    bool rx_stop_ = false, dec_idle_ = true;
+    bool rx_stop_ = false, dec_idle_ = true, dec_dead_ = false;
+    std::atomic<bool> fail_decoder_{false};
     std::exception_ptr rx_err_;
     std::thread rx_thread_, dec_thread_;
 };

@@ -54,6 +54,8 @@ def build(force: bool = False, verbose: bool = False) -> pathlib.Path:
         if verbose:
             print(" ".join(link), flush=True)
         subprocess.check_call(link)
+        from psyne_amd.srchash import write_record
+        write_record(LIB, ARCH, HIPCC)  # (the key PMC traffic records are matched by)
     return LIB
 
 

@@ -1575,7 +1575,10 @@ int ensure_one(tdt_ctx *c, size_t bytes) {
     c->one = nullptr;
     c->one_bytes = 0;
     const size_t cap = std::max<size_t>(bytes, 64 * 1024);
-    HIPCHK(hipHostMalloc(&c->one, cap, hipHostMallocDefault));
+    // coherent (fine-grained, uncached on the device): the kernel's result stores reach host
+    // memory before the stream writes the completion word the host spins on, with no cache
+    // write-back to order; the block is read and written once per call anyway
+    HIPCHK(hipHostMalloc(&c->one, cap, hipHostMallocCoherent));
     c->one_bytes = cap;
     return TDT_OK;
 }

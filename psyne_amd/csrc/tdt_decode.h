@@ -259,6 +259,15 @@ struct FastHdr {
 // starts inside the blob begins at block b0[r] of stream r — the 512-pair block holding
 // position g_lo·seg_r - 1, whose first pair starts at s0[r] (the scan's prefix); kNone: the
 // stream ends before the tile (s0 = its length).
+// pair-block dword loads (PSY_DEC_LDNT: non-temporal)
+__device__ __forceinline__ uint32_t gload_blk(const uint32_t *p) {
+#ifdef PSY_DEC_LDNT
+    return __builtin_nontemporal_load((const __attribute__((address_space(1))) uint32_t *)(p));
+#else
+    return gload<uint32_t>(p);
+#endif
+}
+
 template <int WR_ = kDecWR>
 __device__ __forceinline__ void decode_fast(const FastHdr &H, uint8_t *smem, const uint8_t *blob, const uint8_t *blim,
                                             uint8_t *dst, uint32_t ngroups, uint64_t wbytes, uint32_t g_lo = 0,
@@ -338,12 +347,11 @@ __device__ __forceinline__ void decode_fast(const FastHdr &H, uint8_t *smem, con
             const uint8_t *sb = blob + soff[r];
             const uint32_t sh = (uint32_t)__builtin_amdgcn_readfirstlane((int)((uintptr_t)sb & 3u));
             const uint32_t *q = reinterpret_cast<const uint32_t *>(((uintptr_t)sb & ~(uintptr_t)3) + 2ull * p0);
-            const uint32_t w0 = gload<uint32_t>(q), w1 = gload<uint32_t>(q + 1), w2 = gload<uint32_t>(q + 2),
-                           w3 = gload<uint32_t>(q + 3);
+            const uint32_t w0 = gload_blk(q), w1 = gload_blk(q + 1), w2 = gload_blk(q + 2), w3 = gload_blk(q + 3);
             if (sh == 0u) {
                 pv = make_uint4(w0, w1, w2, w3);
             } else {
-                const uint32_t w4 = gload<uint32_t>(q + 4);
+                const uint32_t w4 = gload_blk(q + 4);
                 pv = make_uint4(__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
                                 __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh));
             }

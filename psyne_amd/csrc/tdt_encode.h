@@ -154,7 +154,10 @@ struct EncLayout {
     static constexpr int WSTAGE_V5 = 256 + 4 * (2 + 64 * 16);
     // v6 (u16 entries): NB rounds per flush — 3 for message-sized teams (fewer flushes, the LDS
     // fits 3 workgroups per CU), 2 for the one-wave team (whose LDS sets messages per CU)
-    static constexpr int NB6 = TEAM >= 256 ? 3 : 2;
+#ifndef PSY_ENC_NB6
+#define PSY_ENC_NB6 3
+#endif
+    static constexpr int NB6 = TEAM >= 256 ? PSY_ENC_NB6 : 2;
     static constexpr int WSTAGE_V6 = 16 + 2 * (3 + NB6 * 64 * 16);
     static constexpr int WSTAGE_45 = WSTAGE_V4 > WSTAGE_V5 ? WSTAGE_V4 : WSTAGE_V5;
     static constexpr int WSTAGE = ((WSTAGE_45 > WSTAGE_V6 ? WSTAGE_45 : WSTAGE_V6) + 15) / 16 * 16;
@@ -337,6 +340,10 @@ __device__ __forceinline__ uint32_t spread2(uint32_t e) {
 // Occupancy target (min waves per SIMD): 3 workgroups of 512 per CU = 6 waves per SIMD.
 #ifndef PSY_ENC_WPE
 #define PSY_ENC_WPE 6
+#endif
+// cache policy of the resident message loads (raw buffer loads; gfx950: 2 = nt)
+#ifndef PSY_ENC_LDAUX
+#define PSY_ENC_LDAUX 0
 #endif
 #define PSY_ENC_WAVES(TEAM) ((TEAM) >= 256 ? PSY_ENC_WPE : 7)
 
@@ -524,14 +531,16 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
         // Raw buffer loads over the message (num_records = n): the round offsets are scalar
         // and lanes past the end read zeros from the hardware range check, so no per-round
         // address arithmetic (round 4: a compare, a select and a 64-bit address per round);
-        // every pass masks those lanes by vbytes / vmask.
+        // every pass masks those lanes by vbytes / vmask.  (A resident message is whole 16-byte
+        // groups, n % 16 == 0, so num_records = n = ngroups·16: the range check never splits a
+        // dword — ADVICE r05 asked.)
         const __amdgpu_buffer_rsrc_t rsrc =
             __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(base), (short)0, (int)n32, 0x00020000);
         const int vo = (int)((gw0 + (uint32_t)lane) * 16u);
 #pragma unroll
         for (int r = 0; r < G; ++r) {
             typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
-            const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, vo, r * 1024, 0);
+            const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, vo, r * 1024, PSY_ENC_LDAUX);
             dres[r] = make_uint4(v.x, v.y, v.z, v.w);
             cres[r] = 0;
         }

@@ -7,7 +7,8 @@
 //   * reference decode errors keep the reference's text ("Invalid TDT magic number");
 //   * after receive_batch started the pipeline with a small max_msg, a frame larger than its
 //     buffers (and than the decoder's limit) still reaches transport_receive intact (ADVICE r04:
-//     the receiver used to hand Inner a too-small buffer, which drops the connection).
+//     the receiver used to hand Inner a too-small buffer, which drops the connection);
+//   * a failed decoder thread surfaces as an exception from transport_receive, not a hang.
 // Prints "cpp substrate OK" on success.
 #include <psyne_amd/tdt_substrate.hpp>
 
@@ -106,6 +107,24 @@ int main() {
 
     // 5. default construction (ChannelBridge: std::make_unique<SubstrateType>())
     static_assert(std::is_default_constructible_v<TdtSubstrate<PosixTcpSubstrate>>);
+
+    // 6. (last: it stops the pipeline) the decoder thread fails on the next buffer, as a failed
+    //    GPU decode call does: transport_receive throws the decoder's error instead of waiting
+    //    forever for the frames it never decoded
+    rx.fail_next_decode_for_test();
+    raw.transport_send(blob.data(), blob.size());
+    raw.transport_send(b2.data(), b2.size());
+    threw = false;
+    {
+        const auto t0 = std::chrono::steady_clock::now();
+        try {
+            rx.transport_receive(buf.data(), buf.size());
+        } catch (const std::runtime_error &e) {
+            threw = std::string(e.what()).find("injected") != std::string::npos;
+        }
+        CHECK(std::chrono::steady_clock::now() - t0 < std::chrono::seconds(10), "decoder failure reported promptly");
+    }
+    CHECK(threw, "decoder failure reaches transport_receive");
     std::printf("cpp substrate OK name=%s\n", rx.substrate_name());
     return 0;
 }

@@ -30,8 +30,11 @@
 // --procs 2 runs the receiving end in a child process forked before anything touches the GPU, so
 // each end has its own process, HIP context and hardware queues, as the two hosts' ends of a link
 // would (they still share this host's GPU, PCIe link and cores); the child reports its end time
-// (CLOCK_MONOTONIC, shared by both processes) and its mismatch count through a pipe.  One JSON line
-// on stdout.
+// (CLOCK_MONOTONIC, shared by both processes) and its mismatch count through a pipe.  --passes P
+// repeats the timed pass P times back to back on the same connection (each pass's clock runs from
+// its first send to its last verified receive; the next pass starts after that), and reports
+// every pass's rate with their median, minimum and maximum: one pass of C1 is ~0.1 s of traffic,
+// too short to tell two rows apart.  One JSON line on stdout.
 #include <dlfcn.h>
 #include <sys/prctl.h>
 #include <sys/wait.h>
@@ -41,6 +44,7 @@
 
 #include <psyne_amd/tdt_substrate.hpp>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -93,6 +97,7 @@ int main(int argc, char **argv) {
     // (tdt_host_alloc: the GPU row's encode DMAs them directly instead of staging them)
     std::string mem = "pageable";
     int port = 18080, procs = 1;
+    size_t passes = 1;
     std::string codec = "gpu", dump;
     for (int i = 1; i + 1 < argc; i += 2) {
         const std::string k = argv[i], v = argv[i + 1];
@@ -107,6 +112,7 @@ int main(int argc, char **argv) {
         else if (k == "--rx") rxmode = v;
         else if (k == "--mem") mem = v;
         else if (k == "--procs") procs = std::stoi(v);
+        else if (k == "--passes") passes = std::max<size_t>(1, std::stoul(v));
     }
     // --procs 2: fork before any thread exists and before anything touches the GPU (pinned
     // payloads included); role "tx" = the parent (sender), "rx" = the child (receiver)
@@ -367,10 +373,14 @@ int main(int argc, char **argv) {
         if (rx) rx0 = rx->pipe_stats();
     }
     if (role == "rx") {
-        // warm-up done (the parent starts its clock on this report), then the timed pass
+        // warm-up done (the parent starts its clock on this report), then the timed passes, each
+        // ended by a report
         if (!send_report()) return 6;
-        pass(count, nullptr);
-        const bool ok = send_report();
+        bool ok = true;
+        for (size_t k = 0; k < passes && ok; ++k) {
+            pass(count, nullptr);
+            ok = send_report();
+        }
         if (codec == "gpu") {
             const PS r = rx->pipe_stats();
             std::fprintf(stderr,
@@ -394,17 +404,26 @@ int main(int argc, char **argv) {
         std::fprintf(stderr, "receiver process ended during the warm-up (exit %d)\n", reap());
         return 6;
     }
-    const auto t0 = std::chrono::steady_clock::now();
-    pass(count, frames);
-    double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    if (role == "tx") {
-        // the receiving end's last verified receive ends the clock
-        if (!read_report(rr)) {
-            std::fprintf(stderr, "receiver process ended without its report (exit %d)\n", reap());
-            return 6;
+    std::vector<double> pass_secs;
+    for (size_t k = 0; k < passes; ++k) {
+        const auto t0 = std::chrono::steady_clock::now();
+        pass(count, k == 0 ? frames : nullptr);
+        double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (role == "tx") {
+            // the receiving end's last verified receive of the pass ends its clock
+            if (!read_report(rr)) {
+                std::fprintf(stderr, "receiver process ended without its report (exit %d)\n", reap());
+                return 6;
+            }
+            secs = (double)(rr.t_ns - std::chrono::duration_cast<std::chrono::nanoseconds>(t0.time_since_epoch()).count()) *
+                   1e-9;
+            mismatches = (size_t)rr.mismatches;
         }
-        secs = (double)(rr.t_ns - std::chrono::duration_cast<std::chrono::nanoseconds>(t0.time_since_epoch()).count()) * 1e-9;
-        mismatches = (size_t)rr.mismatches;
+        pass_secs.push_back(secs);
+    }
+    double secs = 0;
+    for (double x : pass_secs) secs += x;
+    if (role == "tx") {
         const int code = reap();
         if (code != 0 && code != 1) {
             std::fprintf(stderr, "receiver process exit %d\n", code);
@@ -414,16 +433,27 @@ int main(int argc, char **argv) {
     if (frames) std::fclose(frames);
     if (ref_tx) ref.release(ref_tx);
     if (ref_rx) ref.release(ref_rx);
-    const double orig = double(count) * double(bytes);
+    const double orig1 = double(count) * double(bytes), orig = orig1 * double(passes);
+    // per-pass rates, their median / min / max; effective_MBps is the median pass
+    std::vector<double> rate;
+    for (double x : pass_secs) rate.push_back(orig1 / 1e6 / x);
+    std::vector<double> sorted = rate;
+    std::sort(sorted.begin(), sorted.end());
+    const size_t P = sorted.size();
+    const double median = P % 2 ? sorted[P / 2] : 0.5 * (sorted[P / 2 - 1] + sorted[P / 2]);
+    std::string rates = "[";
+    for (size_t k = 0; k < P; ++k) rates += (k ? ", " : "") + std::to_string((long long)(rate[k] + 0.5));
+    rates += "]";
     std::printf("{\"harness\": \"tcp_loopback\", \"codec\": \"%s\", \"tensors\": %zu, \"tensor_bytes\": %zu, "
-                "\"batch\": %zu, \"seconds\": %.4f, \"original_MB\": %.1f, \"wire_MB\": %.1f, "
-                "\"compression_ratio\": %.4f, \"effective_MBps\": %.1f, \"network_MBps\": %.1f, "
+                "\"batch\": %zu, \"passes\": %zu, \"seconds\": %.4f, \"original_MB\": %.1f, \"wire_MB\": %.1f, "
+                "\"compression_ratio\": %.4f, \"effective_MBps\": %.1f, \"min_MBps\": %.1f, \"max_MBps\": %.1f, "
+                "\"pass_MBps\": %s, \"network_MBps\": %.1f, "
                 "\"mismatches\": %zu, \"warmup_tensors\": %zu, \"half\": \"%s\", \"rx\": \"%s\", \"mem\": \"%s\", "
                 "\"procs\": %d}\n",
-                codec.c_str(), count, bytes, codec == "gpu" ? batch : (size_t)1, secs, orig / 1e6,
-                double(wire) / 1e6, orig / double(wire), orig / 1e6 / secs, double(wire) / 1e6 / secs, mismatches,
-                warm ? std::min(count, warm * batch) : (size_t)0, half.c_str(), codec == "gpu" ? rxmode.c_str() : "-",
-                mem.c_str(), procs == 2 ? 2 : 1);
+                codec.c_str(), count, bytes, codec == "gpu" ? batch : (size_t)1, P, secs, orig / 1e6,
+                double(wire) / 1e6, orig / double(wire), median, sorted.front(), sorted.back(), rates.c_str(),
+                double(wire) / 1e6 / secs, mismatches, warm ? std::min(count, warm * batch) : (size_t)0, half.c_str(),
+                codec == "gpu" ? rxmode.c_str() : "-", mem.c_str(), procs == 2 ? 2 : 1);
     if (codec == "gpu" && role == "tx") {
         const PS t = tx->pipe_stats();
         std::fprintf(stderr,

@@ -493,6 +493,54 @@ def test_decode_crafted_fast_path(orc):
         assert got[i] == want, f"crafted blob {i}"
 
 
+def test_every_ws4_mapping_device_decode(orc):
+    """Every one of the 16 word-size-4 byte-plane mappings through the device encoder
+    (tdt_encode_with_mapping_batch) and the device decoder's recombine forms (12+4, 4+12, 8+8
+    bits, one stream; `[1,1,1,1]` leaves stream 0 empty): blobs byte for byte against the
+    oracle's encode with that mapping, then the device's blobs decoded on the device against
+    the oracle's decode (status and bytes) and the input (recombine_byte_streams :614-637).
+    Sizes 1 KiB (one-wave decode), 64 KiB, 100,000 B and 100,004 B (a partial last 16-byte
+    group), 1 MiB (tiled decode); gradient-like and uniform bytes."""
+    rng = np.random.default_rng(606)
+    maps = [[(mb >> b) & 1 for b in range(4)] for mb in range(16)]
+    msgs, mapping = [], []
+    for mp in maps:
+        for n in (1024, 65536, 100000, 100004, 1 << 20):
+            for kind in ("grad", "uniform"):
+                if kind == "uniform" and n > 65536:
+                    continue  # (incompressible large blobs add bytes, not decode forms)
+                m = grad(rng, n // 4) if kind == "grad" else rng.integers(0, 256, n, dtype=np.uint8)
+                msgs.append(np.ascontiguousarray(m))
+                mapping.append(mp)
+    codec = make_codec()
+    buf, off = pack(msgs)
+    mp_t = torch.tensor(np.array(mapping, np.int32).reshape(-1)).cuda()
+    enc, eoff, st = codec.encode_batch(torch.from_numpy(buf).cuda(), torch.from_numpy(off).cuda(), mapping=mp_t)
+    torch.cuda.synchronize()
+    e, eo, st = enc.cpu().numpy(), eoff.cpu().numpy(), st.cpu().numpy()
+    cfg = orc.config(word_size=4)
+    blobs = []
+    for i, (m, mp) in enumerate(zip(msgs, mapping)):
+        want = orc.encode(m, cfg=cfg, mapping=mp)
+        got = e[eo[i]:eo[i + 1]].tobytes()
+        assert int(st[i]) == 0, (i, mp, len(m))
+        assert got == want, f"encode, mapping {mp}, n={len(m)}"
+        blobs.append(got)
+    dec, dst = decode_list(codec, blobs)
+    for i, (m, mp) in enumerate(zip(msgs, mapping)):
+        s, want = orc.decode(blobs[i])
+        assert dst[i] == s == 0, (i, mp, len(m), dst[i], s)
+        assert dec[i] == want == bytes(m), f"decode, mapping {mp}, n={len(m)}"
+    # every blob up to 256 KiB once more through tdt_decode_host with one message per call: the
+    # one-message kernels (one wave up to 4 KiB, the 16-wave tiled kernel above)
+    for i, b in enumerate(blobs):
+        if len(msgs[i]) > 256 * 1024:
+            continue
+        arr = np.frombuffer(b, np.uint8)
+        d1, _, s1 = codec.decode_host(arr, np.array([0, arr.size], np.uint64), len(msgs[i]))
+        assert s1[0] == 0 and d1.tobytes() == bytes(msgs[i]), f"one-message decode, mapping {mapping[i]}, n={len(msgs[i])}"
+
+
 @pytest.mark.parametrize("n", [0, 1, 8191, 8192, 8193, 20000, 50001])
 def test_slot_offsets_multi_chunk(n):
     """tdt_encode_slots (closed form) and tdt_decode_slots (two-pass chunked scan, 8192

@@ -125,6 +125,27 @@ def test_bench_two_ranks_shared_device(launcher):
     assert r["value"] > 0 and r["cpu_baseline"] is None
 
 
+@pytest.mark.timeout(300)
+def test_bench_eight_ranks_shared_device():
+    """8-rank rehearsal of the driver's SCALE point: `bench.py --gpus 8`
+    starts eight ranks itself; on this one-GPU box they share device 0 (PSYNE_BENCH_SHARED_DEVICE),
+    each with its own 4,096-message C3 shard, and rank 0 prints one line with eight per-rank
+    entries and a checked round trip.  (The driver's own --gpus 8 run on an 8-GPU node gives each
+    rank its own GPU; nothing else differs.)"""
+    env = dict(os.environ, PSYNE_BENCH_SHARED_DEVICE="1", OMP_NUM_THREADS="2")
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, "bench.py", "--gpus", "8", "--msgs", "4096", "--steps", "2", "--warmup", "1",
+           "--cpu-seconds", "0", "--compacted-steps", "0"]
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=280)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    r = json.loads(lines[0])
+    assert r["n_gpus"] == 8 and r["world_size_observed"] == 8 and r["roundtrip_ok"] is True
+    assert [x["rank"] for x in r["per_rank"]] == list(range(8))
+    assert r["scaling"] == "weak" and r["value"] > 0
+
+
 @pytest.mark.timeout(240)
 def test_topology_on_the_box():
     """The launcher's topology helpers on a real MI355X box (round 4 reported

@@ -63,11 +63,10 @@ def main():
                     "hbm_bytes_per_launch": tot / calls, "calls": calls}
     lib = pathlib.Path(sys.argv[4] if len(sys.argv) > 4 else
                        pathlib.Path(__file__).resolve().parent.parent / "psyne_amd" / "libpsyne_tdt.so")
-    default_lib = len(sys.argv) <= 4 and not os.environ.get("PSYNE_TDT_LIB")
     sys.path.insert(0, str(pathlib.Path(__file__).resolve().parent.parent))
-    from psyne_amd.srchash import src_sha256
+    from psyne_amd.srchash import recorded
     res = {"config": key, "kernels": kernels, "lib_sha256": hashlib.sha256(lib.read_bytes()).hexdigest(),
-           "src_sha256": src_sha256() if default_lib else None,
+           "src_sha256": recorded(lib),  # (written by the build beside the library; None for variants)
            "method": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950 correction) and WRITE_SIZE in separate passes"}
     with open(out, "w") as f:
         json.dump(res, f, indent=1)
