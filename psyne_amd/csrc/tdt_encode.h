@@ -154,10 +154,12 @@ struct EncLayout {
     static constexpr int WSTAGE_V5 = 256 + 4 * (2 + 64 * 16);
     // v6 (u16 entries): NB rounds per flush — 3 for message-sized teams (fewer flushes, the LDS
     // fits 3 workgroups per CU), 2 for the one-wave team (whose LDS sets messages per CU)
+    // (512-lane teams: 2 rounds of staging, so that the team's LDS (38.3 KB) lets four teams share
+    // a CU — 8 waves per SIMD, round 6 — where 3 rounds (50.9 KB) allowed three)
 #ifndef PSY_ENC_NB6
-#define PSY_ENC_NB6 3
+#define PSY_ENC_NB6 2
 #endif
-    static constexpr int NB6 = TEAM >= 256 ? PSY_ENC_NB6 : 2;
+    static constexpr int NB6 = TEAM >= 512 ? PSY_ENC_NB6 : TEAM >= 256 ? 3 : 2;
     static constexpr int WSTAGE_V6 = 16 + 2 * (3 + NB6 * 64 * 16);
     static constexpr int WSTAGE_45 = WSTAGE_V4 > WSTAGE_V5 ? WSTAGE_V4 : WSTAGE_V5;
     static constexpr int WSTAGE = ((WSTAGE_45 > WSTAGE_V6 ? WSTAGE_45 : WSTAGE_V6) + 15) / 16 * 16;
@@ -337,15 +339,18 @@ __device__ __forceinline__ uint32_t spread2(uint32_t e) {
 // LB = 1: compacted output, offsets by decoupled look-back (out_off written);
 // LB = 0: slotted output at caller offsets (slot_off), lengths to out_len — no dependency
 //         between messages.
-// Occupancy target (min waves per SIMD): 3 workgroups of 512 per CU = 6 waves per SIMD.
+// Occupancy target (min waves per SIMD) of the 512-lane teams: 4 workgroups per CU = 8 waves per
+// SIMD (64 VGPRs; round 6: the C3 encode 7.44 -> 7.29 ms against 6 waves at 73 VGPRs, same box,
+// alternating runs; its 8-VGPR spill is stored in pass A1 and reloaded in pass B, 3 dwords per
+// lane).  The 256-lane teams stay at 6: their LDS (26 KB) allows no more.
 #ifndef PSY_ENC_WPE
-#define PSY_ENC_WPE 6
+#define PSY_ENC_WPE 8
 #endif
 // cache policy of the resident message loads (raw buffer loads; gfx950: 2 = nt)
 #ifndef PSY_ENC_LDAUX
 #define PSY_ENC_LDAUX 0
 #endif
-#define PSY_ENC_WAVES(TEAM) ((TEAM) >= 256 ? PSY_ENC_WPE : 7)
+#define PSY_ENC_WAVES(TEAM) ((TEAM) >= 512 ? PSY_ENC_WPE : (TEAM) >= 256 ? 6 : 7)
 
 // One message — or, TL > 0, part of a large message: TL 1 the histogram of one span of
 // kSpanTiles tiles (UNCP messages: the span's copy), 4 the mapping from the message's span
@@ -1747,15 +1752,20 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
                 pos6[q] = ((x & 0x7f7f7f7fu) + jq) ^ (x & 0x80808080u);
             }
         }
+        // a round's chunk starts: this lane's exclusive rank and the round's total per stream
+        // (packed: stream 1 in the high half).  Taken before the round's sweep, so that a batch is
+        // flushed only when THIS round's entries would not fit (round 6: the worst-case test,
+        // 64·Ls entries per round, flushed C3's 8 rounds three times with 2-round staging)
+        auto scan6 = [&](uint32_t C, uint32_t &pexc, uint32_t &Stot) __attribute__((always_inline)) {
+            const uint32_t pc = popc(C & lowX) | (popc(C & highX) << 16);
+            const uint32_t pinc = wave_incl_scan<OpAdd>(pc);
+            pexc = pinc - pc;
+            Stot = __builtin_amdgcn_readfirstlane(rdlane(pinc, 63));
+        };
         // C in the byte-lane layout for the resident body (BL), compact for the streaming one
-        auto sweep6 = [&](const uint4 &Tw, uint32_t C) __attribute__((always_inline)) {
+        auto sweep6 = [&](const uint4 &Tw, uint32_t C, uint32_t pexc, uint32_t Stot) __attribute__((always_inline)) {
             PSY_ASM_ROUND(B);
             const uint32_t T[4] = {Tw.x, Tw.y, Tw.z, Tw.w};
-            const uint32_t c0 = popc(C & lowX);
-            const uint32_t pc = c0 | (popc(C & highX) << 16);
-            const uint32_t pinc = wave_incl_scan<OpAdd>(pc);
-            const uint32_t pexc = pinc - pc;
-            const uint32_t Stot = rdlane(pinc, 63);
             // entry 0 of a region holds the pending chunk (when there is one); the batch's own
             // entries follow it
             const uint32_t D0 = eb6 + 2u * ((hp[0] ? 1u : 0u) + s6[0] + (pexc & 0xffffu)) - jl;
@@ -1866,10 +1876,10 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
 
         if constexpr (RES) {
           if constexpr (E6) {
-            // A batch of rounds is flushed when the next round could overflow a stream's staging
-            // region (capacity: the pending entry + NB rounds of 64·Ls entries), or at the
-            // wave's last round — 2 flushes for a C3 message's 8 rounds where a fixed NB = 3
-            // took 3.
+            // A batch of rounds is flushed before a round whose entries would overflow a stream's
+            // staging region (capacity: the pending entry + NB rounds of 64·Ls entries; the
+            // round's own count, scan6), and at the wave's last round — 2 flushes for a C3
+            // message's 8 rounds.
             const uint32_t cap6[2] = {1u + NB * 64u * Ls[0], 1u + NB * 64u * Ls[1]};
             bool fresh = true;
             bool resolved = false;
@@ -1924,30 +1934,40 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
                 return __builtin_amdgcn_readfirstlane(ok) != 0u;
             };
             uint32_t rb = 0;  // the batch's first round
+            // flush the batch of rounds [rb, re)
+            auto flush_batch = [&](uint32_t re) __attribute__((always_inline)) -> bool {
+                if constexpr (DEFER) {
+                    if (!resolved) {
+                        resolved = true;
+                        if (!resolve_lb()) return false;  // TDT_E_CAPACITY: nothing is written
+                    }
+                }
+                const uint32_t gb = gw0 + rb * 64u, ge = gw0 + re * 64u;
+                flush6(gb <= ngroups - 1 && ngroups - 1 < ge);
+                fresh = true;
+                rb = re;
+                return true;
+            };
 #pragma unroll
             for (int r = 0; r < G; ++r) {
                 if ((uint32_t)r < RW) {
+                    uint32_t pexc, Stot;
+                    scan6(cres[r], pexc, Stot);
+                    const bool over = (hp[0] ? 1u : 0u) + s6[0] + (Stot & 0xffffu) > cap6[0] ||
+                                      (ns2 && (hp[1] ? 1u : 0u) + s6[1] + (Stot >> 16) > cap6[1]);
+                    if (over && !fresh) {
+                        if (!flush_batch((uint32_t)r)) return;
+                    }
                     if (fresh && lane == 0) {  // batch start: the pending entries
                         if (hp[0]) *reinterpret_cast<uint16_t *>(smem + eb6) = (uint16_t)pend6[0];
                         if (ns2 && hp[1]) *reinterpret_cast<uint16_t *>(smem + eb6 + eoff6) = (uint16_t)pend6[1];
                     }
                     fresh = false;
 #ifndef PSY_X_NOEMIT
-                    sweep6(dres[r], cres[r]);
+                    sweep6(dres[r], cres[r], pexc, Stot);
 #endif
-                    const bool over = (hp[0] ? 1u : 0u) + s6[0] + 64u * Ls[0] > cap6[0] ||
-                                      (ns2 && (hp[1] ? 1u : 0u) + s6[1] + 64u * Ls[1] > cap6[1]);
-                    if (over || (uint32_t)(r + 1) == RW) {
-                        if constexpr (DEFER) {
-                            if (!resolved) {
-                                resolved = true;
-                                if (!resolve_lb()) return;  // TDT_E_CAPACITY: nothing is written
-                            }
-                        }
-                        const uint32_t gb = gw0 + rb * 64u, ge = gw0 + (uint32_t)r * 64u + 64u;
-                        flush6(gb <= ngroups - 1 && ngroups - 1 < ge);
-                        fresh = true;
-                        rb = (uint32_t)r + 1u;
+                    if ((uint32_t)(r + 1) == RW) {
+                        if (!flush_batch((uint32_t)r + 1u)) return;
                     }
                 }
             }
@@ -1988,15 +2008,23 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
                     uint4 Tn = make_uint4(0, 0, 0, 0);
                     uint32_t Cn = 0;
                     if (r + 1 < RW) Cn = chunk_of(r + 1, load_group(gw0 + (r + 1) * 64 + lane), Tn);
+                    uint32_t pexc, Stot;
+                    scan6(Cc, pexc, Stot);
+                    const bool over = (hp[0] ? 1u : 0u) + s6[0] + (Stot & 0xffffu) > cap6[0] ||
+                                      (ns2 && (hp[1] ? 1u : 0u) + s6[1] + (Stot >> 16) > cap6[1]);
+                    if (over && !fresh) {  // this round's entries would not fit: flush [rb, r) first
+                        const uint32_t gb = gw0 + rb * 64u, ge = gw0 + r * 64u;
+                        flush6(gb <= ngroups - 1 && ngroups - 1 < ge);
+                        fresh = true;
+                        rb = r;
+                    }
                     if (fresh && lane == 0) {  // batch start: the pending entries
                         if (hp[0]) *reinterpret_cast<uint16_t *>(smem + eb6) = (uint16_t)pend6[0];
                         if (ns2 && hp[1]) *reinterpret_cast<uint16_t *>(smem + eb6 + eoff6) = (uint16_t)pend6[1];
                     }
                     fresh = false;
-                    sweep6(Tc, Cc);
-                    const bool over = (hp[0] ? 1u : 0u) + s6[0] + 64u * Ls[0] > cap6[0] ||
-                                      (ns2 && (hp[1] ? 1u : 0u) + s6[1] + 64u * Ls[1] > cap6[1]);
-                    if (over || r + 1 == RW) {
+                    sweep6(Tc, Cc, pexc, Stot);
+                    if (r + 1 == RW) {
                         const uint32_t gb = gw0 + rb * 64u, ge = gw0 + r * 64u + 64u;
                         flush6(gb <= ngroups - 1 && ngroups - 1 < ge);
                         fresh = true;

@@ -13,7 +13,7 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 on() { [[ $PHASES == *" $1 "* ]] && echo "== $1"; }
 if on tests; then
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > "$OUT/gpu_tests.log" 2>&1
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > "$OUT/gpu_tests.log" 2>&1
 rc=$?; tail -2 "$OUT/gpu_tests.log"; [ $rc -eq 0 ] || exit $rc
 fi
 if on smoke; then

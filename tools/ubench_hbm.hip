@@ -73,9 +73,12 @@ __global__ __launch_bounds__(B) void k_chunk(const u32x4 *__restrict__ src, u32x
     for (int g = 0; g < G; ++g)
         v[g] = LNT ? __builtin_nontemporal_load(src + base + (uint64_t)g * B + threadIdx.x)
                    : src[base + (uint64_t)g * B + threadIdx.x];
-    // (a little work, so the compiler cannot forward loads to stores)
+    // (a little work, so the compiler cannot forward loads to stores; the pieces not stored are
+    // folded into the first stored one so that every load stays live)
 #pragma unroll
     for (int g = 0; g < G; ++g) v[g] = v[g] ^ (u32x4){(unsigned)g, 0u, 0u, 0u};
+#pragma unroll
+    for (int g = G * WN / 8; g < G; ++g) v[0] ^= v[g];
     const uint64_t ob = (uint64_t)blockIdx.x * B * G * WN / 8;
 #pragma unroll
     for (int g = 0; g < G * WN / 8; ++g) {
