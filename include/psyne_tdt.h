@@ -188,6 +188,13 @@ void tdt_host_free(void *ptr);
 /* dst[0, bytes) = src[0, bytes) on the context's staging-copy threads (a parallel memcpy: one
  * thread's copy is below what a socket pipeline needs).  Host memory only. */
 int tdt_host_copy(tdt_ctx *ctx, void *dst, const void *src, uint64_t bytes);
+/* d_dst[0, bytes) = d_src[0, bytes) between device buffers, asynchronously on hip_stream (NULL:
+ * the null stream), by the codec's hand-written HBM copy: one 512-lane workgroup per 64 KiB piece,
+ * every load of the piece in flight before its non-temporal stores — the access shape of the
+ * resident encode / decode, and the best hand-written copy measured on MI355X (tools/ubench_hbm.hip:
+ * 5.6-5.8 TB/s read + write).  bench.py times it as roofline.copy_ceiling.  Any sizes and
+ * alignments; the buffers must not overlap. */
+int tdt_copy_device(void *d_dst, const void *d_src, uint64_t bytes, void *hip_stream);
 
 /* Device-side invariant flags: bit0 look-back timeout, bit1 staging-index guard, bit2
  * flush-bound guard.  Always 0 for a correct build; the guards turn a logic error into a flag

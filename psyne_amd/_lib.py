@@ -54,6 +54,7 @@ SIGNATURES = {
     "tdt_host_alloc": (C.c_int, [C.c_uint64, C.POINTER(C.c_void_p)]),
     "tdt_host_free": (None, [_vp]),
     "tdt_host_copy": (C.c_int, [_vp, _vp, _vp, C.c_uint64]),
+    "tdt_copy_device": (C.c_int, [_vp, _vp, C.c_uint64, _vp]),
     "tdt_analyze_host": (C.c_int, [_vp, _vp, _vp, C.c_uint32, _vp, _vp, _vp]),
     "tdt_ctx_error_flags": (C.c_int, [_vp, _vp, C.POINTER(C.c_uint32)]),
     "tdt_ctx_set_option": (C.c_int, [_vp, C.c_int, C.c_uint64]),

@@ -541,6 +541,23 @@ def test_every_ws4_mapping_device_decode(orc):
         assert s1[0] == 0 and d1.tobytes() == bytes(msgs[i]), f"one-message decode, mapping {mapping[i]}, n={len(msgs[i])}"
 
 
+def test_copy_device():
+    """tdt_copy_device (the hand-written HBM copy bench.py reports as roofline.copy_ceiling):
+    every size class (byte head / 64 KiB pieces / partial last piece / byte tail) at equal and
+    unequal 16-byte phases, nothing written outside [dst, dst + n)."""
+    from psyne_amd._lib import check, load
+    lib = load()
+    rng = np.random.default_rng(77)
+    src = torch.from_numpy(rng.integers(0, 256, (3 << 20) + 64, dtype=np.uint8)).cuda()
+    for n in (0, 1, 15, 16, 17, 4095, 65536, 65536 * 3 + 17, (3 << 20) - 5):
+        for so, do in ((0, 0), (3, 3), (5, 9), (16, 0)):
+            dst = torch.full(((3 << 20) + 128,), 0xA5, dtype=torch.uint8, device="cuda")
+            check(lib.tdt_copy_device(dst.data_ptr() + do, src.data_ptr() + so, n, None))
+            torch.cuda.synchronize()
+            assert torch.equal(dst[do:do + n], src[so:so + n]), (n, so, do)
+            assert int((dst[:do] != 0xA5).sum()) == 0 and int((dst[do + n:] != 0xA5).sum()) == 0, (n, so, do)
+
+
 @pytest.mark.parametrize("n", [0, 1, 8191, 8192, 8193, 20000, 50001])
 def test_slot_offsets_multi_chunk(n):
     """tdt_encode_slots (closed form) and tdt_decode_slots (two-pass chunked scan, 8192
