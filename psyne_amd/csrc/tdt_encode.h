@@ -350,7 +350,10 @@ __device__ __forceinline__ uint32_t spread2(uint32_t e) {
 #ifndef PSY_ENC_LDAUX
 #define PSY_ENC_LDAUX 0
 #endif
-#define PSY_ENC_WAVES(TEAM) ((TEAM) >= 512 ? PSY_ENC_WPE : (TEAM) >= 256 ? 6 : 7)
+#ifndef PSY_ENC_WPE_LB
+#define PSY_ENC_WPE_LB 6
+#endif
+#define PSY_ENC_WAVES(TEAM, LB) ((TEAM) >= 512 ? ((LB) ? PSY_ENC_WPE_LB : PSY_ENC_WPE) : (TEAM) >= 256 ? 6 : 7)
 
 // One message — or, TL > 0, part of a large message: TL 1 the histogram of one span of
 // kSpanTiles tiles (UNCP messages: the span's copy), 4 the mapping from the message's span
@@ -2085,7 +2088,7 @@ __device__ __forceinline__ uint32_t entry_count(const EncodeArgs &a) {
 }
 
 template <int WS, int TEAM, int G, int MODE, int LB, int TL = 0, int PS = 0, int PATH = PATH_BOTH>
-__global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM)) void tdt_encode_kernel(EncodeArgs a) {
+__global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM, LB)) void tdt_encode_kernel(EncodeArgs a) {
     using Lay = EncLayout<WS, TEAM>;
     constexpr int W = Lay::W;
     __shared__ __attribute__((aligned(16))) uint8_t smem[Lay::BYTES];
