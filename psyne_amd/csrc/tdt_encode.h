@@ -387,13 +387,16 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
     const uint64_t off0 = a.in_off[msg];
     const uint64_t n = a.in_off[msg + 1] - off0;
     const uint8_t *base = a.in + off0;
-    // slotted outputs: the slot is known now; loading it here keeps its latency off the
-    // critical path between the count pass and the emit pass
+    // slotted outputs: the slot bounds are loaded where they are used (round 6: loaded here, at
+    // the start, they stayed live through every pass — four SGPRs that the 8-wave register
+    // budget spilled and reloaded in the emit rounds)
     uint64_t slot_b = 0, slot_e = 0;
-    if constexpr (!LB) {
-        slot_b = a.slot_off[msg];
-        slot_e = a.slot_off[msg + 1];
-    }
+    auto load_slot = [&]() __attribute__((always_inline)) {
+        if constexpr (!LB) {
+            slot_b = a.slot_off[msg];
+            slot_e = a.slot_off[msg + 1];
+        }
+    };
 
     // Output placement of an E-byte result (all threads call it): returns the offset in
     // a.out and whether the result fits.
@@ -416,6 +419,7 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
                 if (msg == a.n_msgs - 1) a.out_off[a.n_msgs] = ob + E;
             }
         } else {
+            load_slot();
             ob = slot_b;
             fits = E <= slot_e - ob;
             if (tid == 0 && a.out_len) a.out_len[msg] = fits ? E : 0;
@@ -440,6 +444,7 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
     if (!compress) {
         if constexpr (TL == 1) {
             const uint64_t E = n + 4;
+            load_slot();
             const bool fits = E <= slot_e - slot_b;
             if (tile == 0 && tid == 0) {
                 if (a.status) a.status[msg] = fits ? ST_OK : ST_CAPACITY;
@@ -1532,6 +1537,7 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
         if constexpr (TL == 3) {
             const LMeta *lm = a.lmeta + lj;
             if (!lm->fits) return;  // the scan gave the message CAPACITY
+            load_slot();
             ob = slot_b;
             P0m = lm->P0;
             pin[0] += tr->cnt[0];  // chunk starts before the tile
@@ -1733,7 +1739,10 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
         // entries are dword-aligned for the flush)
         constexpr uint32_t NB = Lay::NB6;  // rounds per flush
         const uint32_t eoff6 = 2u * (2u + NB * 64u * L0);
-        uint32_t s6[2] = {0, 0};  // entries of the current batch, per stream
+        // entries staged per stream: the pending chunk (entry 0, when there is one) plus the
+        // batch's own (round 6: one integer, so that the flush tests stay on the scalar unit —
+        // the pending flag as a bool came out as v_cndmask / v_cmp per round)
+        uint32_t u6[2] = {hp[0] ? 1u : 0u, hp[1] ? 1u : 0u};
         uint32_t pend6[2] = {0, 0};
 #pragma unroll
         for (int c = 0; c < 2; ++c) pend6[c] = ((pend[c] >> 24) << 8) | ((pend[c] - 256u + gw0 * Ls[c]) & 0xffu);
@@ -1771,8 +1780,8 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
             const uint32_t T[4] = {Tw.x, Tw.y, Tw.z, Tw.w};
             // entry 0 of a region holds the pending chunk (when there is one); the batch's own
             // entries follow it
-            const uint32_t D0 = eb6 + 2u * ((hp[0] ? 1u : 0u) + s6[0] + (pexc & 0xffffu)) - jl;
-            const uint32_t D1 = eb6 + eoff6 + 2u * ((hp[1] ? 1u : 0u) + s6[1] + (pexc >> 16)) - jl;
+            const uint32_t D0 = eb6 + 2u * (u6[0] + (pexc & 0xffffu)) - jl;
+            const uint32_t D1 = eb6 + eoff6 + 2u * (u6[1] + (pexc >> 16)) - jl;
             uint32_t D = L0 == 0 ? D1 : D0;
             // entries of slots q + 4t, two per dword: E[q][0] = slots q, q+4; E[q][1] = q+8, q+12
             uint32_t E[4][2];
@@ -1787,25 +1796,25 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
                 if (j > 0 && j % WPG == 0 && (uint32_t)j == L0) D = D1;  // stream 1 begins (uniform)
                 const uint32_t bit = (C >> (BL ? sb_pos(j) : j)) & 1u;
                 uint32_t ad;
-                asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(ad) : "v"(bit), "v"(D), "v"(jl));
+                asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(ad) : "v"(bit), "v"(D), "s"(jl));
                 const uint32_t e = E[q][t >> 1];
                 if (t & 1) *reinterpret_cast<uint16_t *>(smem + ad) = (uint16_t)(e >> 16);
                 else *reinterpret_cast<uint16_t *>(smem + ad) = (uint16_t)e;
                 asm("v_lshl_add_u32 %0, %1, 1, %2" : "=v"(D) : "v"(bit), "v"(D));
             }
-            s6[0] += Stot & 0xffffu;
-            s6[1] += Stot >> 16;
+            u6[0] += Stot & 0xffffu;
+            u6[1] += Stot >> 16;
         };
         // flush the batch; last: the stream ends in it
         auto flush6 = [&](bool last) __attribute__((always_inline)) {
 #if defined(PSY_X_NOEMIT) || defined(PSY_X_NOFLUSH)
-            if (ngroups != 0xffffffffu) { s6[0] = s6[1] = 0; return; }  // diagnostic: no flush
+            if (ngroups != 0xffffffffu) { u6[0] = u6[1] = 0; return; }  // diagnostic: no flush
 #endif
             team_sync<1>();
 #pragma unroll
             for (int c = 0; c < 2; ++c) {
                 if (c == 1 && !ns2) break;
-                const uint32_t nent = s6[c] + (hp[c] ? 1u : 0u);
+                const uint32_t nent = u6[c];
                 const uint32_t K = nent ? nent - 1u : 0u;  // pair k = entries k, k + 1
                 const uint32_t eb = eb6 + (c ? eoff6 : 0u);
                 uint8_t *const Dp = dst + sdata[c] + 2ull * pi5[c];
@@ -1870,9 +1879,8 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
                         pi5[c] += 1;
                     }
                     pend6[c] = el;
-                    hp[c] = true;
                 }
-                s6[c] = 0;
+                u6[c] = nent ? 1u : 0u;
             }
             team_sync<1>();  // the entries are rewritten by the next batch
         };
@@ -1956,14 +1964,14 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
                 if ((uint32_t)r < RW) {
                     uint32_t pexc, Stot;
                     scan6(cres[r], pexc, Stot);
-                    const bool over = (hp[0] ? 1u : 0u) + s6[0] + (Stot & 0xffffu) > cap6[0] ||
-                                      (ns2 && (hp[1] ? 1u : 0u) + s6[1] + (Stot >> 16) > cap6[1]);
-                    if (over && !fresh) {
+                    const uint32_t over = (u6[0] + (Stot & 0xffffu) > cap6[0] ? 1u : 0u) |
+                                          (u6[1] + (Stot >> 16) > cap6[1] ? 1u : 0u);
+                    if (over != 0u && !fresh) {
                         if (!flush_batch((uint32_t)r)) return;
                     }
                     if (fresh && lane == 0) {  // batch start: the pending entries
-                        if (hp[0]) *reinterpret_cast<uint16_t *>(smem + eb6) = (uint16_t)pend6[0];
-                        if (ns2 && hp[1]) *reinterpret_cast<uint16_t *>(smem + eb6 + eoff6) = (uint16_t)pend6[1];
+                        if (u6[0]) *reinterpret_cast<uint16_t *>(smem + eb6) = (uint16_t)pend6[0];
+                        if (ns2 && u6[1]) *reinterpret_cast<uint16_t *>(smem + eb6 + eoff6) = (uint16_t)pend6[1];
                     }
                     fresh = false;
 #ifndef PSY_X_NOEMIT
@@ -2013,17 +2021,17 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
                     if (r + 1 < RW) Cn = chunk_of(r + 1, load_group(gw0 + (r + 1) * 64 + lane), Tn);
                     uint32_t pexc, Stot;
                     scan6(Cc, pexc, Stot);
-                    const bool over = (hp[0] ? 1u : 0u) + s6[0] + (Stot & 0xffffu) > cap6[0] ||
-                                      (ns2 && (hp[1] ? 1u : 0u) + s6[1] + (Stot >> 16) > cap6[1]);
-                    if (over && !fresh) {  // this round's entries would not fit: flush [rb, r) first
+                    const uint32_t over = (u6[0] + (Stot & 0xffffu) > cap6[0] ? 1u : 0u) |
+                                          (u6[1] + (Stot >> 16) > cap6[1] ? 1u : 0u);
+                    if (over != 0u && !fresh) {  // this round's entries would not fit: flush [rb, r) first
                         const uint32_t gb = gw0 + rb * 64u, ge = gw0 + r * 64u;
                         flush6(gb <= ngroups - 1 && ngroups - 1 < ge);
                         fresh = true;
                         rb = r;
                     }
                     if (fresh && lane == 0) {  // batch start: the pending entries
-                        if (hp[0]) *reinterpret_cast<uint16_t *>(smem + eb6) = (uint16_t)pend6[0];
-                        if (ns2 && hp[1]) *reinterpret_cast<uint16_t *>(smem + eb6 + eoff6) = (uint16_t)pend6[1];
+                        if (u6[0]) *reinterpret_cast<uint16_t *>(smem + eb6) = (uint16_t)pend6[0];
+                        if (ns2 && u6[1]) *reinterpret_cast<uint16_t *>(smem + eb6 + eoff6) = (uint16_t)pend6[1];
                     }
                     fresh = false;
                     sweep6(Tc, Cc, pexc, Stot);
