@@ -387,16 +387,14 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
     const uint64_t off0 = a.in_off[msg];
     const uint64_t n = a.in_off[msg + 1] - off0;
     const uint8_t *base = a.in + off0;
-    // slotted outputs: the slot bounds are loaded where they are used (round 6: loaded here, at
-    // the start, they stayed live through every pass — four SGPRs that the 8-wave register
-    // budget spilled and reloaded in the emit rounds)
+    // slotted outputs: the slot is known now; loading it here keeps its latency off the
+    // critical path between the count pass and the emit pass (round 6: loaded at its first use
+    // instead, the C3 encode took 8.2-8.7 ms against 7.26)
     uint64_t slot_b = 0, slot_e = 0;
-    auto load_slot = [&]() __attribute__((always_inline)) {
-        if constexpr (!LB) {
-            slot_b = a.slot_off[msg];
-            slot_e = a.slot_off[msg + 1];
-        }
-    };
+    if constexpr (!LB) {
+        slot_b = a.slot_off[msg];
+        slot_e = a.slot_off[msg + 1];
+    }
 
     // Output placement of an E-byte result (all threads call it): returns the offset in
     // a.out and whether the result fits.
@@ -419,7 +417,6 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
                 if (msg == a.n_msgs - 1) a.out_off[a.n_msgs] = ob + E;
             }
         } else {
-            load_slot();
             ob = slot_b;
             fits = E <= slot_e - ob;
             if (tid == 0 && a.out_len) a.out_len[msg] = fits ? E : 0;
@@ -444,7 +441,6 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
     if (!compress) {
         if constexpr (TL == 1) {
             const uint64_t E = n + 4;
-            load_slot();
             const bool fits = E <= slot_e - slot_b;
             if (tile == 0 && tid == 0) {
                 if (a.status) a.status[msg] = fits ? ST_OK : ST_CAPACITY;
@@ -1537,7 +1533,6 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
         if constexpr (TL == 3) {
             const LMeta *lm = a.lmeta + lj;
             if (!lm->fits) return;  // the scan gave the message CAPACITY
-            load_slot();
             ob = slot_b;
             P0m = lm->P0;
             pin[0] += tr->cnt[0];  // chunk starts before the tile
