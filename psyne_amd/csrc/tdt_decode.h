@@ -343,7 +343,6 @@ __device__ __forceinline__ void decode_fast(const FastHdr &H, uint8_t *smem, con
         // holds a byte of the next pair: no bounds tests) — else the checked, zero-filled load
         const bool full = bidx[r] + 512u < np[r];
         uint4 pv;
-        uint32_t nvb = 8u;  // valid pairs of this lane (the last block: fewer)
         if (full) {
             const uint8_t *sb = blob + soff[r];
             const uint32_t sh = (uint32_t)__builtin_amdgcn_readfirstlane((int)((uintptr_t)sb & 3u));
@@ -358,7 +357,6 @@ __device__ __forceinline__ void decode_fast(const FastHdr &H, uint8_t *smem, con
             }
         } else {
             const uint32_t nv = p0 < np[r] ? (np[r] - p0 < 8u ? np[r] - p0 : 8u) : 0u;
-            nvb = nv;
             pv = nv ? ld16_span(blob + soff[r] + 2ull * p0, (int)(2 * nv), blim) : make_uint4(0, 0, 0, 0);
         }
         const uint32_t pw[4] = {pv.x, pv.y, pv.z, pv.w};
@@ -374,18 +372,6 @@ __device__ __forceinline__ void decode_fast(const FastHdr &H, uint8_t *smem, con
 #ifndef PSY_X_NOCOUNTED
         if (full) {
             const uint32_t mn = pk_min_u16(pk_min_u16(cw[0], cw[1]), pk_min_u16(cw[2], cw[3]));
-            counted = !__any((mn & 0xffffu) == 0u || (mn >> 16) == 0u);
-        } else {
-            // the stream's last block (round 6): only its valid pairs need a count.  The zero-filled
-            // pairs past the stream's end (count 0, value 0) all start AT its end, so their key can
-            // only mark positions >= the stream length, which hold zeros anyway (recombine
-            // :626-631: a stream that ran short leaves zeros; the fill masks them) or lie past the
-            // message; every C2 blob's streams end in a partial block
-            uint32_t t[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-                t[j] = cw[j] | (2u * j >= nvb ? 1u : 0u) | (2u * j + 1u >= nvb ? 0x10000u : 0u);
-            const uint32_t mn = pk_min_u16(pk_min_u16(t[0], t[1]), pk_min_u16(t[2], t[3]));
             counted = !__any((mn & 0xffffu) == 0u || (mn >> 16) == 0u);
         }
 #endif
