@@ -98,6 +98,15 @@ struct DecLayoutT {
     static constexpr int GBYTES = OFF_MISC + MISC;
     static constexpr int BYTES = OFF_FHEADS + FHEADS > GBYTES ? OFF_FHEADS + FHEADS : GBYTES;
     static_assert(kHdrCache + 16 <= GHEADS && kHdrCache + 16 <= FHEADS, "header cache inside the heads");
+    // One-round windows (the small-blob list): the fast path's heads end at 2128 and the generic
+    // path writes only MISC before its heads, so [OFF_BLOB, OFF_MISC) holds the blob's first
+    // BLOBC bytes for the whole decode — a blob of up to BLOBC bytes is read from HBM in ONE trip
+    // and its header, stream table and pair blocks come from LDS (no extra LDS per wave).
+    static constexpr int OFF_BLOB = WR == 1 ? 2144 : OFF_HDR;
+    static constexpr int BLOBC = WR == 1 ? OFF_MISC - OFF_BLOB : kHdrCache;
+    static_assert(WR != 1 || (OFF_BLOB >= OFF_FHEADS + FHEADS && OFF_BLOB % 16 == 0 && BLOBC % 4 == 0 &&
+                              OFF_BLOB + BLOBC + 20 <= BYTES),
+                  "blob cache beside the fast path's heads, before MISC (+20: a pair block's 5-dword over-read)");
 };
 using DecLayout = DecLayoutT<>;
 
@@ -271,7 +280,8 @@ __device__ __forceinline__ uint32_t gload_blk(const uint32_t *p) {
 template <int WR_ = kDecWR>
 __device__ __forceinline__ void decode_fast(const FastHdr &H, uint8_t *smem, const uint8_t *blob, const uint8_t *blim,
                                             uint8_t *dst, uint32_t ngroups, uint64_t wbytes, uint32_t g_lo = 0,
-                                            uint32_t g_hi = 0, const uint32_t *b0 = nullptr, const uint32_t *s0 = nullptr) {
+                                            uint32_t g_hi = 0, const uint32_t *b0 = nullptr, const uint32_t *s0 = nullptr,
+                                            const uint8_t *bc = nullptr, uint32_t bcl = 0) {
     using Lay = DecLayoutT<WR_>;
     constexpr uint32_t WR = WR_;
     const uint32_t lane = (uint32_t)lane_id();
@@ -315,6 +325,10 @@ __device__ __forceinline__ void decode_fast(const FastHdr &H, uint8_t *smem, con
         sd_off[d] = sd_pb[d] + lane * sd_mul[d];
     }
 
+    // streams held whole in the LDS blob cache (bc: the blob's first bcl bytes, decode_one's
+    // small-blob list): their pair blocks are LDS reads, not dependent HBM trips
+    const bool cached[2] = {bc != nullptr && soff[0] + 2u * np[0] <= bcl, bc != nullptr && soff[1] + 2u * np[1] <= bcl};
+
     // per stream block state (uniform) and registers (per lane)
     uint32_t bidx[2] = {0u, 0u};      // pair index of the NEXT block to load
     uint32_t bend[2] = {0u, 0u};      // absolute end position of the loaded block
@@ -343,7 +357,32 @@ __device__ __forceinline__ void decode_fast(const FastHdr &H, uint8_t *smem, con
         // holds a byte of the next pair: no bounds tests) — else the checked, zero-filled load
         const bool full = bidx[r] + 512u < np[r];
         uint4 pv;
-        if (full) {
+        if (cached[r]) {
+            // 5 dword LDS reads + alignbyte; past the stream's end the bytes are zeroed (a lane
+            // without pairs reads the block's first, in-range, bytes)
+            const uint32_t nv = full ? 8u : (p0 < np[r] ? (np[r] - p0 < 8u ? np[r] - p0 : 8u) : 0u);
+            const uint32_t sh = soff[r] & 3u;
+            const uint32_t *q =
+                reinterpret_cast<const uint32_t *>(bc + (soff[r] & ~3u) + 2u * (nv ? p0 : bidx[r]));
+            const uint32_t w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3];
+            if (sh == 0u) {
+                pv = make_uint4(w0, w1, w2, w3);
+            } else {
+                const uint32_t w4 = q[4];
+                pv = make_uint4(__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
+                                __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh));
+            }
+            if (!full) {
+                const uint32_t vb = 2u * nv;  // valid bytes (even: 0, 2 or 4 per dword)
+                uint32_t m[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const uint32_t kq = vb <= 4u * j ? 0u : (vb - 4u * j >= 4u ? 4u : vb - 4u * j);
+                    m[j] = kq >= 4u ? 0xffffffffu : ((1u << (8u * kq)) - 1u);
+                }
+                pv = make_uint4(pv.x & m[0], pv.y & m[1], pv.z & m[2], pv.w & m[3]);
+            }
+        } else if (full) {
             const uint8_t *sb = blob + soff[r];
             const uint32_t sh = (uint32_t)__builtin_amdgcn_readfirstlane((int)((uintptr_t)sb & 3u));
             const uint32_t *q = reinterpret_cast<const uint32_t *>(((uintptr_t)sb & ~(uintptr_t)3) + 2ull * p0);
@@ -876,31 +915,48 @@ template <int LB, int WR = kDecWR>
 __device__ __forceinline__ void decode_one(const DecodeArgs &a, uint8_t *smem, uint32_t msg) {
     using Lay = DecLayoutT<WR>;
     uint32_t *misc = reinterpret_cast<uint32_t *>(smem + Lay::OFF_MISC);
-    uint8_t *hdrc = smem + Lay::OFF_HDR;
+    uint8_t *hdrc = smem + Lay::OFF_BLOB;
     const int lane = lane_id();
     PSY_PROF_BEGIN();
     if (msg >= a.n_msgs) return;
     const uint64_t boff = a.in_off[msg];
     const uint64_t len = a.in_len ? a.in_len[msg] : a.in_off[msg + 1] - boff;
+    // the slot is read beside the offsets (it depends on msg only): one dependent trip fewer
+    uint64_t slot_b = 0, slot_e = 0;
+    if constexpr (!LB) {
+        slot_b = a.slot_off[msg];
+        slot_e = a.slot_off[msg + 1];
+    }
     const uint8_t *blob = a.in + boff;
     const uint8_t *blim = blob + len;
 
-    // ------------------------------------------------ header cache: first 256 bytes in LDS
+    // ------------------------------------------------ blob cache: its first BLOBC bytes in LDS
+    // (256 with the main list's windows; 1504 with one-round windows, whole small blobs)
+    constexpr uint32_t BLOBC = (uint32_t)Lay::BLOBC;
+    const uint32_t hcl = len < (uint64_t)BLOBC ? (uint32_t)len : BLOBC;
     {
-        const uint64_t hc = len < (uint64_t)kHdrCache ? len : (uint64_t)kHdrCache;
-        const uint32_t o = (uint32_t)lane * 4u;
-        uint32_t w = 0;
-        if (((uintptr_t)blob & 3) == 0 && o + 4 <= hc) {
-            w = *reinterpret_cast<const uint32_t *>(blob + o);  // one dword per lane
-        } else {
+        constexpr int ND = (int)((BLOBC / 4 + 63) / 64);  // dwords per lane
+        uint32_t w[ND];
+        const bool al4 = ((uintptr_t)blob & 3) == 0;
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
-                if (o + i < hc) w |= (uint32_t)blob[o + i] << (8 * i);
+        for (int j = 0; j < ND; ++j) {  // (all loads issued before the first LDS write)
+            const uint32_t o = ((uint32_t)lane + 64u * (uint32_t)j) * 4u;
+            w[j] = 0;
+            if (al4 && o + 4 <= hcl) {
+                w[j] = *reinterpret_cast<const uint32_t *>(blob + o);
+            } else if (o < hcl) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    if (o + i < hcl) w[j] |= (uint32_t)blob[o + i] << (8 * i);
+            }
         }
-        reinterpret_cast<uint32_t *>(hdrc)[lane] = w;
+#pragma unroll
+        for (int j = 0; j < ND; ++j) {
+            const uint32_t d = (uint32_t)lane + 64u * (uint32_t)j;
+            if (d < BLOBC / 4) reinterpret_cast<uint32_t *>(hdrc)[d] = w[j];
+        }
     }
     team_sync<1>();
-    const uint32_t hcl = len < (uint64_t)kHdrCache ? (uint32_t)len : (uint32_t)kHdrCache;
 
     // ------------------------------------------------ fast path (wave-parallel header parse)
     const FastHdr H = parse_fast(blob, len, hdrc, hcl);
@@ -912,8 +968,8 @@ __device__ __forceinline__ void decode_one(const DecodeArgs &a, uint8_t *smem, u
             ob = lookback_excl_wave(a.lookback, msg, osize, a.errflags);
             fits = ob + osize <= a.out_cap;
         } else {
-            ob = a.slot_off[msg];
-            fits = osize <= a.slot_off[msg + 1] - ob;
+            ob = slot_b;
+            fits = osize <= slot_e - ob;
         }
         const uint32_t st = fits ? ST_OK : ST_CAPACITY;
         if (lane == 0) {
@@ -934,7 +990,8 @@ __device__ __forceinline__ void decode_one(const DecodeArgs &a, uint8_t *smem, u
         const uint64_t wbytes = (uint64_t)(H.orig / H.ws) * H.ws;
         // recombine :617 zero-initialises; bytes past the last whole word stay zero
         if (H.orig > wbytes) team_zero<64>(dst + wbytes, H.orig - wbytes);
-        decode_fast<WR>(H, smem, blob, blim, dst, (uint32_t)((wbytes + 15) / 16), wbytes);
+        decode_fast<WR>(H, smem, blob, blim, dst, (uint32_t)((wbytes + 15) / 16), wbytes, 0, 0, nullptr, nullptr,
+                        WR == 1 ? hdrc : nullptr, WR == 1 ? hcl : 0u);
         return;
     }
     auto rd32 = [&](uint64_t off) -> uint32_t {
@@ -1034,8 +1091,8 @@ __device__ __forceinline__ void decode_one(const DecodeArgs &a, uint8_t *smem, u
         ob = lookback_excl_wave(a.lookback, msg, osize, a.errflags);
         fits = ob + osize <= a.out_cap;
     } else {
-        ob = a.slot_off[msg];
-        fits = osize <= a.slot_off[msg + 1] - ob;
+        ob = slot_b;
+        fits = osize <= slot_e - ob;
     }
     if (st == ST_OK && !fits) st = ST_CAPACITY;
     if (lane == 0) {
@@ -1743,8 +1800,12 @@ __global__ __launch_bounds__(64, LB ? 6 : 8) void tdt_decode_kernel(DecodeArgs a
                 decode_one<LB, WR>(a, smem, entry(i));
             }
         } else {
+            // the list entries are read beside the counts, not after them (i0 < n_msgs = every
+            // list's capacity; a stale entry past the count is never used): one dependent trip
+            const uint32_t ic = i0 < a.n_msgs ? i0 : a.n_msgs - 1u;
+            const uint32_t eb = a.blist ? a.blist[ic] : 0u, el = a.list[ic];
             if (i0 >= cnt) return;
-            decode_one<LB, WR>(a, smem, entry(i0));
+            decode_one<LB, WR>(a, smem, i0 < nb ? eb : (nb == 0u ? el : a.list[i0 - nb]));
         }
     }
 }

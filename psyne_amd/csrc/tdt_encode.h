@@ -2124,6 +2124,14 @@ __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM, LB)) void tdt_encode_kern
                 if (i != i0) team_sync<W>();  // the previous entry is done with the LDS
                 one(i);
             }
+        } else if constexpr (TL == 0) {
+            // the list entry is read beside the counts, not after them (i0 < n_msgs = every
+            // class list's capacity; a stale entry past the count is never used)
+            const uint32_t ic = i0 < a.n_msgs ? i0 : a.n_msgs - 1u;
+            const uint32_t e2 = a.list2 ? a.list2[ic] : 0u, e1 = a.list[ic];
+            if (i0 >= cnt) return;
+            encode_one<WS, TEAM, G, MODE, LB, 0, PATH>(a, smem, i0 < n2 ? e2 : (n2 == 0u ? e1 : a.list[i0 - n2]), 0,
+                                                       0);
         } else {
             if (i0 >= cnt) return;
             one(i0);
