@@ -126,7 +126,7 @@ struct EncodeArgs {
     unsigned long long *rcount;
 };
 
-template <int WS, int TEAM>
+template <int WS, int TEAM, int LB = 0>
 struct EncLayout {
     static constexpr int W = TEAM / 64;
     static constexpr int WPG = 16 / WS;  // words per 16-byte group
@@ -159,7 +159,13 @@ struct EncLayout {
 #ifndef PSY_ENC_NB6
 #define PSY_ENC_NB6 2
 #endif
-    static constexpr int NB6 = TEAM >= 512 ? PSY_ENC_NB6 : TEAM >= 256 ? 3 : 2;
+// (the compacted look-back instances run at 6 waves per SIMD, three teams per CU: they keep 3
+// rounds of staging — their first flush, where the team waits for its offset, comes a round
+// later: C3 compacted encode 9.36-9.41 -> 8.80-8.82 ms, profiles/r06_bc/ab_compact/lb3/)
+#ifndef PSY_ENC_NB6_LB
+#define PSY_ENC_NB6_LB 3
+#endif
+    static constexpr int NB6 = TEAM >= 512 ? (LB ? PSY_ENC_NB6_LB : PSY_ENC_NB6) : TEAM >= 256 ? 3 : 2;
     static constexpr int WSTAGE_V6 = 16 + 2 * (3 + NB6 * 64 * 16);
     static constexpr int WSTAGE_45 = WSTAGE_V4 > WSTAGE_V5 ? WSTAGE_V4 : WSTAGE_V5;
     static constexpr int WSTAGE = ((WSTAGE_45 > WSTAGE_V6 ? WSTAGE_45 : WSTAGE_V6) + 15) / 16 * 16;
@@ -369,7 +375,7 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
                                            uint32_t tile) {
     static_assert(TL == 0 || (TEAM * G == (int)kTileGroups && MODE == MODE_ENCODE && !LB), "tile shape");
     constexpr uint32_t kTG = TL == 1 ? kTileGroups * kSpanTiles : kTileGroups;  // groups per team
-    using Lay = EncLayout<WS, TEAM>;
+    using Lay = EncLayout<WS, TEAM, LB>;
     constexpr int W = Lay::W;
     constexpr int WPG = Lay::WPG;
     uint32_t *slots = reinterpret_cast<uint32_t *>(smem + Lay::OFF_SLOTS);
@@ -1895,7 +1901,11 @@ __device__ __forceinline__ void encode_one(const EncodeArgs &a, uint8_t *smem, u
                 uint64_t b;
                 uint32_t ok;
                 if (wv == 0) {
+#ifndef PSY_X_NOLBWAIT
                     b = lookback_resolve(a.lookback, msg, Eblob, a.errflags);
+#else
+                    b = (uint64_t)msg * (28 + 4 * WS + 2ull * n);  // diagnostic: offsets without the look-back
+#endif
                     ok = b + Eblob <= a.out_cap ? 1u : 0u;
                     uint8_t *hd = a.out + b;
                     if (lane == 0) {
@@ -2092,7 +2102,7 @@ __device__ __forceinline__ uint32_t entry_count(const EncodeArgs &a) {
 
 template <int WS, int TEAM, int G, int MODE, int LB, int TL = 0, int PS = 0, int PATH = PATH_BOTH>
 __global__ __launch_bounds__(TEAM, PSY_ENC_WAVES(TEAM, LB)) void tdt_encode_kernel(EncodeArgs a) {
-    using Lay = EncLayout<WS, TEAM>;
+    using Lay = EncLayout<WS, TEAM, LB>;
     constexpr int W = Lay::W;
     __shared__ __attribute__((aligned(16))) uint8_t smem[Lay::BYTES];
     if constexpr (LB) {
