@@ -493,6 +493,46 @@ def test_decode_crafted_fast_path(orc):
         assert got[i] == want, f"crafted blob {i}"
 
 
+def test_decode_blob_cache_edges(orc):
+    """The small-blob decode list (blobs decoding to <= 8 KiB) reads each blob's first 1,504
+    bytes into LDS and takes a stream's pair blocks from there when the whole stream lies inside
+    (tdt_decode.h DecLayoutT::BLOBC, decode_fast `cached`).  Blobs whose streams end just before,
+    at and just past that edge — stream 0 stored first or second, one or two streams, even and
+    odd stream lengths, every 4-byte phase of the blob start — against the oracle's decode."""
+    rng = np.random.default_rng(1504)
+    maps = [[1, 1, 0, 0], [0, 1, 1, 1], [0, 1, 0, 1], [0, 0, 0, 0], [1, 0, 0, 0]]
+    blobs = []
+    for i in range(120):
+        mp = maps[i % len(maps)]
+        orig = int(rng.choice([1024, 1100, 2048, 4096, 8192]))
+        ns = max(mp) + 1
+        hdr = struct.pack("<5I", 0x54445444, orig, ns, 4, 4) + struct.pack("<4i", *mp)
+        body = b""
+        for c in range(ns):
+            if c == 0:
+                # the first stored stream ends at blob offset 1504 + d
+                end = 1504 + int(rng.integers(-8, 9))
+                nbytes = end - (len(hdr) + 4)
+            else:
+                nbytes = int(rng.integers(0, 700))
+            k, odd = nbytes // 2, nbytes % 2
+            s = bytearray()
+            for _ in range(k):
+                s += bytes([int(rng.integers(1, 4)), int(rng.integers(0, 256))])
+            if odd:
+                s += bytes([int(rng.integers(1, 256))])
+            body += struct.pack("<I", len(s)) + bytes(s)
+        blobs.append(hdr + body)
+    # (concatenated: the blob starts fall on every phase; a 1-3 byte spacer shifts them further)
+    for lead in (0, 1, 3):
+        got, st = decode_list(make_codec(), ([b"PCNU" + bytes(lead)] if lead else []) + blobs)
+        got, st = (got[1:], st[1:]) if lead else (got, st)
+        for i, b in enumerate(blobs):
+            s, want = orc.decode(b)
+            assert st[i] == s, (lead, i, st[i], s)
+            assert got[i] == want, f"blob {i} (lead {lead}, len {len(b)})"
+
+
 def test_every_ws4_mapping_device_decode(orc):
     """Every one of the 16 word-size-4 byte-plane mappings through the device encoder
     (tdt_encode_with_mapping_batch) and the device decoder's recombine forms (12+4, 4+12, 8+8
