@@ -94,18 +94,25 @@ struct DecLayoutT {
     static constexpr int OFF_HDR = 0;
     static constexpr int OFF_HEADS = 0;
     static constexpr int OFF_GPLANES = GHEADS;
-    static constexpr int OFF_MISC = OFF_GPLANES + PLANES;
+    // One-round windows (the small-blob list): the fast path's heads end at 2128 and the generic
+    // path writes only MISC before its heads, so [OFF_BLOB, OFF_BLOB + BLOBC) holds the blob's
+    // first BLOBC bytes for the whole decode — a blob of up to BLOBC bytes is read from HBM in ONE
+    // trip and its header, stream table and pair blocks come from LDS.  2,112 bytes hold a whole
+    // 1 KiB message's blob at word size 4 (2,092 B when every run has length 1, uniform bytes);
+    // MISC moves past the cache, 5,024 B per wave: still 8 waves per SIMD.
+#ifndef PSY_DEC_BLOBC
+#define PSY_DEC_BLOBC 2112
+#endif
+    static constexpr int OFF_BLOB = WR == 1 ? 2144 : OFF_HDR;
+    static constexpr int BLOBC = WR == 1 ? PSY_DEC_BLOBC : kHdrCache;
+    static constexpr int OFF_MISC = WR == 1 && OFF_BLOB + BLOBC > OFF_GPLANES + PLANES ? OFF_BLOB + BLOBC
+                                                                                      : OFF_GPLANES + PLANES;
     static constexpr int GBYTES = OFF_MISC + MISC;
     static constexpr int BYTES = OFF_FHEADS + FHEADS > GBYTES ? OFF_FHEADS + FHEADS : GBYTES;
     static_assert(kHdrCache + 16 <= GHEADS && kHdrCache + 16 <= FHEADS, "header cache inside the heads");
-    // One-round windows (the small-blob list): the fast path's heads end at 2128 and the generic
-    // path writes only MISC before its heads, so [OFF_BLOB, OFF_MISC) holds the blob's first
-    // BLOBC bytes for the whole decode — a blob of up to BLOBC bytes is read from HBM in ONE trip
-    // and its header, stream table and pair blocks come from LDS (no extra LDS per wave).
-    static constexpr int OFF_BLOB = WR == 1 ? 2144 : OFF_HDR;
-    static constexpr int BLOBC = WR == 1 ? OFF_MISC - OFF_BLOB : kHdrCache;
-    static_assert(WR != 1 || (OFF_BLOB >= OFF_FHEADS + FHEADS && OFF_BLOB % 16 == 0 && BLOBC % 4 == 0 &&
-                              OFF_BLOB + BLOBC + 20 <= BYTES),
+    static_assert(WR != 1 || 32 * ((BYTES + 511) / 512 * 512) <= 160 * 1024, "8 one-wave decodes per SIMD");
+    static_assert(WR != 1 || (OFF_BLOB >= OFF_FHEADS + FHEADS && OFF_BLOB % 16 == 0 && BLOBC % 16 == 0 &&
+                              OFF_BLOB + BLOBC <= OFF_MISC && OFF_BLOB + BLOBC + 20 <= BYTES),
                   "blob cache beside the fast path's heads, before MISC (+20: a pair block's 5-dword over-read)");
 };
 using DecLayout = DecLayoutT<>;
@@ -931,10 +938,35 @@ __device__ __forceinline__ void decode_one(const DecodeArgs &a, uint8_t *smem, u
     const uint8_t *blim = blob + len;
 
     // ------------------------------------------------ blob cache: its first BLOBC bytes in LDS
-    // (256 with the main list's windows; 1504 with one-round windows, whole small blobs)
+    // (256 with the main list's windows; 2,112 with one-round windows: whole 1 KiB-message blobs)
     constexpr uint32_t BLOBC = (uint32_t)Lay::BLOBC;
     const uint32_t hcl = len < (uint64_t)BLOBC ? (uint32_t)len : BLOBC;
-    {
+    if constexpr (BLOBC > 1024) {
+        // 16 bytes per lane and load (dwordx4 at any dword-aligned start; a lane whose 16 bytes
+        // cross the blob's end, or a blob that is not dword-aligned, takes bytes)
+        constexpr int NQ = (int)((BLOBC / 16 + 63) / 64);
+        uint4 q[NQ];
+        const bool al4 = ((uintptr_t)blob & 3) == 0;
+#pragma unroll
+        for (int j = 0; j < NQ; ++j) {  // (all loads issued before the first LDS write)
+            const uint32_t o = ((uint32_t)lane + 64u * (uint32_t)j) * 16u;
+            q[j] = make_uint4(0, 0, 0, 0);
+            if (al4 && o + 16 <= hcl) {
+                typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+                const u32x4_t v = gload<u32x4_t>(blob + o);
+                q[j] = make_uint4(v.x, v.y, v.z, v.w);
+            } else if (o < hcl) {
+                uint32_t w[4] = {0, 0, 0, 0};
+                for (uint32_t i = 0; i < 16 && o + i < hcl; ++i) w[i >> 2] |= (uint32_t)blob[o + i] << (8 * (i & 3));
+                q[j] = make_uint4(w[0], w[1], w[2], w[3]);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < NQ; ++j) {
+            const uint32_t d = (uint32_t)lane + 64u * (uint32_t)j;
+            if (d < BLOBC / 16) reinterpret_cast<uint4 *>(hdrc)[d] = q[j];
+        }
+    } else {
         constexpr int ND = (int)((BLOBC / 4 + 63) / 64);  // dwords per lane
         uint32_t w[ND];
         const bool al4 = ((uintptr_t)blob & 3) == 0;
